@@ -1,0 +1,174 @@
+/*
+ * mkidgpu.h — flat C ABI of the MI355X MKID channeliser + phase/pulse-trigger hot path.
+ *
+ * This library replaces the ROACH FPGA firmware that creanero/MKIDS_SDR configures over katcp
+ * (the firmware itself is absent from the reference: .MISSING_LARGE_BLOBS:1-27). Each entry point
+ * below replaces one group of register/BRAM accesses the reference's host code makes; the
+ * reference call site is cited on every declaration (paths relative to the reference root).
+ *
+ * ABI rules
+ *   - every entry point returns int: 0 = ok, negative = MKID_E_* ; mkid_last_error() gives text.
+ *   - no C++ exception crosses the ABI; buffers are caller-owned; plain pointers and sizes only.
+ *   - one HIP stream per context (its own, or one handed in by mkid_set_stream); a context is not
+ *     thread-safe; distinct contexts (one per GPU / feedline) may run concurrently.
+ *   - *_device entry points take device pointers and are fully asynchronous on the context's
+ *     stream (graph-capturable); the host-pointer entry points copy in/out and synchronise.
+ *
+ * Geometry: C channels, N = 2C point FFT, hop M = N/2 (2x oversampled), T PFB taps per branch.
+ * Input: int16 I/Q pairs (interleaved, I first) at fs. Output: per-channel phase at fs/N
+ * (layout [J][C], time-major, J = nsamples/N) and 64-bit photon packets (see MKID_PKT_*).
+ */
+#ifndef MKIDGPU_H
+#define MKIDGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MKID_OK 0
+#define MKID_E_ARG (-1)       /* bad argument / shape mismatch                      */
+#define MKID_E_HIP (-2)       /* HIP runtime failure (message in mkid_last_error)   */
+#define MKID_E_STATE (-3)     /* call order violated (e.g. process before config)    */
+#define MKID_E_OVERFLOW (-4)  /* event capacity exceeded; events were dropped         */
+#define MKID_E_NODEV (-5)     /* no HIP device                                       */
+
+/* Baseline modes of the trigger (K7). The reference writes these registers:
+ *   capture_Baseline_alpha  (DataReadout/ChannelizerControls/lib/set_alpha.py:10-17, Fix12_9)
+ *   capture_base_Kf/Kq      (lib/set_svf.py:29-35, Fix18_16)
+ *   capture_base_thresh     (lib/set_base_thresh.py:9-17, Fix16_13; B_BASE_THRESH setEnvironment.sh:26) */
+#define MKID_BASE_NONE 0
+#define MKID_BASE_EMA 1
+#define MKID_BASE_SVF 2
+
+/* Wide 64-bit photon packet emitted by the device (channel field widened for C > 255):
+ *   [63:52] channel (12b) | [51:40] peak Fix12_9 offset (x/2^9-4 rad) | [39:28] baseline Fix12_9
+ *   offset | [27:0] phase-sample index mod 2^28.
+ * The reference 64-bit packet (ch 8b | peak 12b | p1 12b | base 12b | ts 20b,
+ * ROACH_Pulses.py:796-832, PacketMaster.c:291-292) is produced on the host by
+ * mkid_pack_reference() for C <= 254. */
+#define MKID_PKT_CH_SHIFT 52
+#define MKID_PKT_PEAK_SHIFT 40
+#define MKID_PKT_BASE_SHIFT 28
+#define MKID_PKT_TS_MASK ((1ull << 28) - 1)
+
+typedef struct mkid_ctx mkid_ctx;
+
+typedef struct mkid_cfg {
+    int32_t n_channels;        /* C; ROACH_Setup.py:515 (256)                                  */
+    int32_t fft_len;           /* N = 2C; ROACH_Setup.py:507 fft_len = 2**9                    */
+    int32_t pfb_taps;          /* T taps per PFB branch (build decision, 4)                    */
+    int32_t fir_taps;          /* 26; ROACH_Pulses.py:61                                      */
+    int32_t dds_entries;       /* P = 2^16 / C LO samples per channel; ROACH_Setup.py:521-530 */
+    int32_t dead_time;         /* trigger dead time in phase samples (build decision)         */
+    int32_t max_events_per_ch; /* per-call event capacity per channel (0 = derive from chunk) */
+    int32_t reserved;
+    int64_t max_chunk;         /* largest nsamples per process call (workspace sizing)        */
+    double sample_rate;        /* fs, complex S/s; ROACH_Setup.py:82                           */
+} mkid_cfg;
+
+/* Fill *cfg with defaults for C channels (N=2C, T=4, 26 taps, P=65536/C, fs=512e6). */
+int mkid_default_cfg(mkid_cfg* cfg, int32_t n_channels);
+
+/* Create a context on HIP device `device`. Replaces FpgaClient(ip,7147)+progdev(bof):
+ * ROACH_Setup.py:112-115, ROACH_Pulses.py:51-52. */
+int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out);
+int mkid_destroy(mkid_ctx* ctx);
+const char* mkid_last_error(const mkid_ctx* ctx);
+/* Error text for failures that happen before a context exists (mkid_create). */
+const char* mkid_global_error(void);
+int mkid_get_cfg(const mkid_ctx* ctx, mkid_cfg* out);
+
+/* Run the context's kernels on an external hipStream_t (e.g. torch's current stream). NULL
+ * restores the context's own stream. */
+int mkid_set_stream(mkid_ctx* ctx, void* hip_stream);
+
+/* PFB prototype filter, T*N float coefficients (build decision: the firmware's taps are not in
+ * the reference). */
+int mkid_set_pfb(mkid_ctx* ctx, const float* coeffs, int32_t n);
+
+/* Coarse FFT bin per channel: replaces write_int('bins'), write_int('load_bins',(i<<1)+1)
+ * (ROACH_Setup.py:534-550; ROACH_Pulses.py:958-974). bins[c] in [0,N). */
+int mkid_set_bins(mkid_ctx* ctx, const int32_t* bins, int32_t n);
+
+/* Per-channel DDS LO LUT, de-interleaved and un-shifted: lut_i/lut_q are [C][P] int16, the
+ * freqCombLUT('no',...) output of define_DDS_LUT (ROACH_Setup.py:506-532) before it is woven
+ * into dram_memory (ROACH_Setup.py:552-570). The device mixes by conj(LUT)/2^15. */
+int mkid_set_dds(mkid_ctx* ctx, const int16_t* lut_i, const int16_t* lut_q, int32_t entries_per_ch);
+
+/* IQ low-pass (K5) taps, int12 Fix12_11 (int(lpf*(2**11-1)), ROACH_Pulses.py:69,88-92), shared
+ * by all channels, applied to the DDC output with decimation by 2. */
+int mkid_set_lpf(mkid_ctx* ctx, const int16_t* taps12, int32_t ntaps);
+
+/* Per-channel matched-filter taps [C][26] int12: replaces FIR_b{2n}b{2n+1} + FIR_load_coeff
+ * (ROACH_Pulses.py:59-111). All-zero taps delete a channel (no triggers). */
+int mkid_set_fir(mkid_ctx* ctx, const int16_t* taps12, int32_t n_channels, int32_t ntaps);
+
+/* IQ loop centres [C] in channel-output units: replaces conv_phase_centers /
+ * conv_phase_load_centers (ROACH_Setup.py:595-605). */
+int mkid_set_centers(mkid_ctx* ctx, const float* ic, const float* qc, int32_t n);
+
+/* Per-channel trigger thresholds [C], Fix16_13 raw units relative to baseline (negative-going):
+ * replaces capture_threshold / capture_load_thresh (ROACH_Pulses.py:211-354). */
+int mkid_set_thresholds(mkid_ctx* ctx, const int32_t* thr, int32_t n);
+
+/* Baseline: mode MKID_BASE_*, alpha Fix12_9, kf/kq Fix18_16, base_thr Fix16_13 (0 = no gate). */
+int mkid_set_baseline(mkid_ctx* ctx, int32_t mode, int32_t alpha, int32_t kf, int32_t kq,
+                      int32_t base_thr);
+
+/* Forget all stream state (PFB/FIR history, baselines, trigger state, sample counter). */
+int mkid_reset_stream(mkid_ctx* ctx);
+
+/* Process nsamples (multiple of N) I/Q pairs, host pointers, synchronous. phase_out (nullable)
+ * receives [nsamples/N][C] float32 rad; events_out receives up to cap packets, channel-major and
+ * time-ascending within a channel; *nevents = packets produced (> cap => MKID_E_OVERFLOW). */
+int mkid_process(mkid_ctx* ctx, const int16_t* iq, int64_t nsamples, float* phase_out,
+                 uint64_t* events_out, int64_t cap, int64_t* nevents);
+
+/* Same with device pointers, asynchronous on the context stream. d_counts is a device int64[2]:
+ * [0] = packets produced (may exceed cap), [1] = packets written. d_phase may be NULL (the phase
+ * stream is then not materialised; the trigger still runs on the Fix16_13 phase). */
+int mkid_process_device(mkid_ctx* ctx, const int16_t* d_iq, int64_t nsamples, float* d_phase,
+                        uint64_t* d_events, int64_t cap, int64_t* d_counts /* [2] */);
+
+/* Fixed-point phase of the last processed call, [J][C] int16 Fix16_13 (the trigger's input),
+ * device pointer valid until the next process call. Replaces the snapPhase_bram source
+ * (ROACH_Pulses.py:357-378). */
+int mkid_last_raw_phase(mkid_ctx* ctx, const int16_t** d_raw, int64_t* nrows);
+
+/* Per-channel mean I/Q of the last processed call (avgIQ_bram, ROACH_Setup.py:654-662), [C] each. */
+int mkid_avg_iq(mkid_ctx* ctx, float* mean_i, float* mean_q);
+
+/* Re-encode wide device packets as the reference 64-bit packet (host memory, C <= 254):
+ *   [63:56] ch | [55:44] peak | [43:32] p1 = peak-base+2048 | [31:20] base | [19:0] ts mod 2^20
+ * (ROACH_Pulses.py:805-832 decode; PacketMaster.c:291-292 assembly; ch 255 = end-of-second). */
+int mkid_pack_reference(const uint64_t* wide, int64_t n, uint64_t* out);
+
+/* Kernel timing with HIP events on the context stream (for bench roofline numbers). */
+#define MKID_K_CHANNELIZE 0
+#define MKID_K_FIR_PHASE 1
+#define MKID_K_TRIGGER 2
+#define MKID_K_COMPACT 3
+#define MKID_K_COUNT 4
+int mkid_set_timing(mkid_ctx* ctx, int32_t enable);
+int mkid_get_timing(mkid_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches);
+const char* mkid_kernel_name(int32_t kernel);
+
+/* Synthetic ADC source for tests/bench (device; NOT part of the hot path):
+ *   out[n] = base[(n0+n) mod 2^16] + AWGN(sigma) + sum_p amp_c e^{i theta_c(t)} (e^{i delta_p(t)} - 1)
+ * base = conj(DAC tone comb) as int16 [2^16][2] (the loop-back spectrum inversion implied by
+ * ROACH_Setup.py:485-487 vs 511-517); theta_c(t) = 2 pi (freq_index_c t mod 2^16)/2^16 + phase0_c;
+ * delta_p(tau) = -amp_rad (1 - e^{-tau/tau_rise}) e^{-tau/tau_fall} for 0 <= tau < window (ADC
+ * samples; shape after ReadoutControls/lib/pulses.py:470-472). pulses sorted by start. */
+typedef struct mkid_synth_tone { float amp; float phase0; int32_t freq_index; int32_t pad; } mkid_synth_tone;
+typedef struct mkid_pulse { int64_t start; int32_t tone; float amp_rad; } mkid_pulse;
+int mkid_synth_adc(mkid_ctx* ctx, int16_t* d_out, int64_t nsamples, int64_t n0,
+                   const int16_t* d_base_iq, const mkid_synth_tone* d_tones,
+                   const mkid_pulse* d_pulses, int64_t npulses, float tau_rise, float tau_fall,
+                   int32_t window, float noise_sigma, uint32_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MKIDGPU_H */

@@ -1,0 +1,161 @@
+"""Python front-end of one MI355X channeliser context (one feedline on one GPU).
+
+This is the host-side mirror of the firmware configuration the reference performs over katcp
+(ROACH_Setup.py / ROACH_Pulses.py) — every setter maps to one register group (see
+include/mkidgpu.h) — and of its data path: ``process`` runs the HIP kernels (PFB+FFT+DDC, IQ
+low-pass + phase, matched-filter trigger) and returns the phase stream and photon packets.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .pfb import pfb_prototype
+
+
+def _ptr(a):
+    """Host numpy array / torch tensor / int -> void*."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    if hasattr(a, 'data_ptr'):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Channelizer:
+    def __init__(self, n_channels, device=0, max_chunk=1 << 22, dead_time=32, sample_rate=512e6,
+                 max_events_per_ch=0):
+        self._L = _lib.load()
+        cfg = _lib.Cfg()
+        _lib.check(self._L.mkid_default_cfg(ctypes.byref(cfg), int(n_channels)))
+        cfg.max_chunk = int(max_chunk)
+        cfg.dead_time = int(dead_time)
+        cfg.sample_rate = float(sample_rate)
+        cfg.max_events_per_ch = int(max_events_per_ch)
+        h = ctypes.c_void_p()
+        _lib.check(self._L.mkid_create(ctypes.byref(cfg), int(device), ctypes.byref(h)))
+        self._h = h
+        self.cfg = cfg
+        self.C = cfg.n_channels
+        self.N = cfg.fft_len
+        self.P = cfg.dds_entries
+        self.set_pfb(pfb_prototype(self.N, cfg.pfb_taps))
+
+    # ---- lifecycle -------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.mkid_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        return _lib.check(rc, self._h)
+
+    # ---- configuration (one register group each) ---------------------------------------------
+    def set_stream(self, stream_ptr):
+        self._chk(self._L.mkid_set_stream(self._h, ctypes.c_void_p(stream_ptr or 0)))
+
+    def set_pfb(self, coeffs):
+        c = np.ascontiguousarray(coeffs, np.float32)
+        self._chk(self._L.mkid_set_pfb(self._h, _ptr(c), c.size))
+
+    def set_bins(self, bins):
+        b = np.ascontiguousarray(bins, np.int32)
+        self._chk(self._L.mkid_set_bins(self._h, _ptr(b), b.size))
+
+    def set_dds(self, lut_i, lut_q):
+        li = np.ascontiguousarray(lut_i, np.int16).reshape(self.C, -1)
+        lq = np.ascontiguousarray(lut_q, np.int16).reshape(self.C, -1)
+        self._chk(self._L.mkid_set_dds(self._h, _ptr(li), _ptr(lq), li.shape[1]))
+
+    def set_lpf(self, taps12):
+        t = np.ascontiguousarray(taps12, np.int16)
+        self._chk(self._L.mkid_set_lpf(self._h, _ptr(t), t.size))
+
+    def set_fir(self, taps12):
+        t = np.ascontiguousarray(taps12, np.int16).reshape(self.C, -1)
+        self._chk(self._L.mkid_set_fir(self._h, _ptr(t), t.shape[0], t.shape[1]))
+
+    def set_centers(self, ic, qc):
+        i = np.ascontiguousarray(ic, np.float32)
+        q = np.ascontiguousarray(qc, np.float32)
+        self._chk(self._L.mkid_set_centers(self._h, _ptr(i), _ptr(q), i.size))
+
+    def set_thresholds(self, thr):
+        t = np.ascontiguousarray(thr, np.int32)
+        self._chk(self._L.mkid_set_thresholds(self._h, _ptr(t), t.size))
+
+    def set_baseline(self, mode=_lib.BASE_EMA, alpha=41, kf=82, kq=93623, base_thr=8192):
+        self._chk(self._L.mkid_set_baseline(self._h, int(mode), int(alpha), int(kf), int(kq),
+                                            int(base_thr)))
+
+    def reset(self):
+        self._chk(self._L.mkid_reset_stream(self._h))
+
+    # ---- data path ---------------------------------------------------------------------------
+    def process(self, iq, want_phase=True, cap=None):
+        """iq: int16 [S][2] host array. Returns (phase [S/N][C] float32 or None, events uint64)."""
+        x = np.ascontiguousarray(iq, np.int16).reshape(-1, 2)
+        S = x.shape[0]
+        J = S // self.N
+        phase = np.empty((J, self.C), np.float32) if want_phase else None
+        cap = J * self.C if cap is None else int(cap)
+        ev = np.empty(max(cap, 1), np.uint64)
+        n = ctypes.c_int64()
+        rc = self._L.mkid_process(self._h, _ptr(x), S, _ptr(phase), _ptr(ev), cap, ctypes.byref(n))
+        self._chk(rc)
+        return phase, ev[:n.value].copy()
+
+    def process_device(self, d_iq, nsamples, d_phase, d_events, cap, d_counts):
+        """Device pointers (ints or torch tensors); asynchronous on the context stream."""
+        self._chk(self._L.mkid_process_device(self._h, _ptr(d_iq), int(nsamples), _ptr(d_phase),
+                                              _ptr(d_events), int(cap), _ptr(d_counts)))
+
+    def raw_phase_ptr(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        self._chk(self._L.mkid_last_raw_phase(self._h, ctypes.byref(p), ctypes.byref(n)))
+        return p.value, n.value
+
+    def avg_iq(self):
+        mi = np.empty(self.C, np.float32)
+        mq = np.empty(self.C, np.float32)
+        self._chk(self._L.mkid_avg_iq(self._h, _ptr(mi), _ptr(mq)))
+        return mi, mq
+
+    # ---- timing ------------------------------------------------------------------------------
+    def set_timing(self, on):
+        self._chk(self._L.mkid_set_timing(self._h, 1 if on else 0))
+
+    def timing(self):
+        out = {}
+        for k in range(_lib.K_COUNT):
+            ms = ctypes.c_double()
+            n = ctypes.c_int64()
+            self._chk(self._L.mkid_get_timing(self._h, k, ctypes.byref(ms), ctypes.byref(n)))
+            out[self._L.mkid_kernel_name(k).decode()] = (ms.value, n.value)
+        return out
+
+    # ---- synthetic source (tests / bench only) -------------------------------------------------
+    def synth_adc(self, d_out, nsamples, n0, d_base, d_tones, d_pulses, npulses, tau_rise,
+                  tau_fall, window, sigma, seed):
+        self._chk(self._L.mkid_synth_adc(self._h, _ptr(d_out), int(nsamples), int(n0),
+                                         _ptr(d_base), _ptr(d_tones), _ptr(d_pulses),
+                                         int(npulses), float(tau_rise), float(tau_fall),
+                                         int(window), float(sigma), int(seed) & 0xffffffff))
+
+
+def pack_reference(wide):
+    """Wide device packets -> reference 64-bit packets (mkid_pack_reference, C <= 254)."""
+    L = _lib.load()
+    w = np.ascontiguousarray(wide, np.uint64)
+    out = np.empty_like(w)
+    _lib.check(L.mkid_pack_reference(_ptr(w), w.size, _ptr(out)))
+    return out

@@ -1,0 +1,152 @@
+// Radix-2/4/8/16 forward DFT butterflies and Stockham LDS passes for the channeliser FFT.
+// Sign convention: X[k] = sum_n x[n] exp(-2 pi i n k / N) (numpy.fft.fft).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mkid {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // -i * a
+
+__device__ __forceinline__ void dft2(float2& a, float2& b) {
+    float2 t = a;
+    a = cadd(t, b);
+    b = csub(t, b);
+}
+
+__device__ __forceinline__ void dft4(float2& v0, float2& v1, float2& v2, float2& v3) {
+    float2 s02 = cadd(v0, v2), d02 = csub(v0, v2);
+    float2 s13 = cadd(v1, v3), d13 = mul_mi(csub(v1, v3));
+    v0 = cadd(s02, s13);
+    v2 = csub(s02, s13);
+    v1 = cadd(d02, d13);
+    v3 = csub(d02, d13);
+}
+
+template <int R>
+__device__ __forceinline__ void dft(float2* v);
+
+template <>
+__device__ __forceinline__ void dft<2>(float2* v) { dft2(v[0], v[1]); }
+
+template <>
+__device__ __forceinline__ void dft<4>(float2* v) { dft4(v[0], v[1], v[2], v[3]); }
+
+template <>
+__device__ __forceinline__ void dft<8>(float2* v) {
+    constexpr float r2 = 0.70710678118654752440f;
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    dft4(e0, e1, e2, e3);
+    dft4(o0, o1, o2, o3);
+    o1 = make_float2((o1.x + o1.y) * r2, (o1.y - o1.x) * r2);   // * W8^1
+    o2 = mul_mi(o2);                                           // * W8^2
+    o3 = make_float2((o3.y - o3.x) * r2, -(o3.x + o3.y) * r2);  // * W8^3
+    v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
+    v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
+    v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
+    v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
+}
+
+template <>
+__device__ __forceinline__ void dft<16>(float2* v) {
+    // n = r + 4m, k = s + 4q: X[s+4q] = sum_r W4^{rq} W16^{rs} sum_m x[r+4m] W4^{ms}
+    constexpr float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+    constexpr float r2 = 0.70710678118654752440f;
+    float2 b[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        b[r][0] = v[r]; b[r][1] = v[r + 4]; b[r][2] = v[r + 8]; b[r][3] = v[r + 12];
+        dft4(b[r][0], b[r][1], b[r][2], b[r][3]);
+    }
+    const float2 w1 = make_float2(c1, -s1), w2 = make_float2(r2, -r2), w3 = make_float2(s1, -c1);
+    b[1][1] = cmul(b[1][1], w1);
+    b[1][2] = cmul(b[1][2], w2);
+    b[1][3] = cmul(b[1][3], w3);
+    b[2][1] = cmul(b[2][1], w2);
+    b[2][2] = mul_mi(b[2][2]);
+    b[2][3] = cmul(b[2][3], make_float2(-r2, -r2));
+    b[3][1] = cmul(b[3][1], w3);
+    b[3][2] = cmul(b[3][2], make_float2(-r2, -r2));
+    b[3][3] = cmul(b[3][3], make_float2(-c1, s1));  // W16^9 = -W16^1
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        float2 a0 = b[0][s], a1 = b[1][s], a2 = b[2][s], a3 = b[3][s];
+        dft4(a0, a1, a2, a3);
+        v[s] = a0; v[s + 4] = a1; v[s + 8] = a2; v[s + 12] = a3;
+    }
+}
+
+// LDS index padding: one float2 of pad every 16 entries (breaks power-of-two lane strides).
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+template <int N>
+constexpr int lds_frame_elems() { return N + N / 16; }
+
+// Stockham pass pieces; thread t of NT = N/PTS threads holds PTS points = PTS/R butterflies.
+template <int N, int PTS, int R>
+__device__ __forceinline__ void st_read(const float2* buf, float2 (&v)[PTS], int t) {
+    constexpr int NT = N / PTS, NB = PTS / R, NR = N / R;
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[q * R + r] = buf[lpad(t + q * NT + r * NR)];
+}
+
+template <int N, int PTS, int R, int NS>
+__device__ __forceinline__ void st_write(float2* buf, const float2 (&v)[PTS], int t) {
+    constexpr int NT = N / PTS, NB = PTS / R;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        const int j = t + q * NT;
+        const int base = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[lpad(base + r * NS)] = v[q * R + r];
+    }
+}
+
+template <int PTS, int R>
+__device__ __forceinline__ void st_dft(float2 (&v)[PTS]) {
+#pragma unroll
+    for (int q = 0; q < PTS / R; ++q) dft<R>(&v[q * R]);
+}
+
+// Twiddles of one pass for this thread's butterflies: w[q][r-1] = exp(-2 pi i (j%NS) r / (NS R)).
+template <int N, int PTS, int R, int NS>
+struct Twiddle {
+    static constexpr int NB = PTS / R;
+    float2 w[NB * (R - 1) > 0 ? NB * (R - 1) : 1];
+    __device__ __forceinline__ void init(int t) {
+        constexpr int NT = N / PTS;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int m = (t + q * NT) % NS;
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                double s, c;
+                sincospi(-2.0 * (double)(m * r) / (double)(NS * R), &s, &c);
+                w[q * (R - 1) + r - 1] = make_float2((float)c, (float)s);
+            }
+        }
+    }
+    __device__ __forceinline__ void apply(float2 (&v)[PTS]) const {
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], w[q * (R - 1) + r - 1]);
+    }
+};
+
+template <int N>
+struct Plan;
+template <> struct Plan<128>  { static constexpr int PTS = 16, NP = 2, R1 = 16, R2 = 8,  R3 = 1; };
+template <> struct Plan<256>  { static constexpr int PTS = 16, NP = 2, R1 = 16, R2 = 16, R3 = 1; };
+template <> struct Plan<512>  { static constexpr int PTS = 8,  NP = 3, R1 = 8,  R2 = 8,  R3 = 8; };
+template <> struct Plan<1024> { static constexpr int PTS = 16, NP = 3, R1 = 16, R2 = 16, R3 = 4; };
+template <> struct Plan<2048> { static constexpr int PTS = 16, NP = 3, R1 = 16, R2 = 16, R3 = 8; };
+template <> struct Plan<4096> { static constexpr int PTS = 16, NP = 3, R1 = 16, R2 = 16, R3 = 16; };
+
+}  // namespace mkid

@@ -1,0 +1,69 @@
+// K5-K6: per-channel 26-tap IQ low-pass with decimation by 2, IQ-centre subtraction, atan2,
+// Fix16_13 quantisation.
+//   y_j = sum_i g_i z_{2j+1-i}                  (taps int(lpf*(2**11-1))/2^11, ROACH_Pulses.py:69,88)
+//   phi_j = atan2(Im y - qc, Re y - ic)          (pulse_triggering_IQ.py:152, conv_phase_centers)
+//   raw_j = clamp(rint(phi_j * 2^13), +-25736)   (Fix16_13, ROACH_Pulses.py:274-278)
+// Thread = one channel x JB consecutive outputs; a 26-deep register window slides by 2 frames.
+#include "fft_common.h"
+#include "mkid_internal.h"
+
+namespace mkid {
+
+constexpr int kLpfThreads = 256;
+constexpr int kLpfJB = 13;  // outputs per thread (window period 26 = 2*13 -> static slots)
+
+__global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
+    const int c = blockIdx.y * kLpfThreads + threadIdx.x;
+    if (c >= a.C) return;
+    const int64_t j0 = (int64_t)blockIdx.x * kLpfJB;
+    const int C = a.C;
+    const float ic = a.ic[c], qc = a.qc[c];
+
+    // window slot s holds z at frame index f with f = s (mod 26) ; start: frames 2*j0+1-25 .. 2*j0
+    float2 w[kFirTaps];
+    const int64_t fbase = 2 * j0 + 1 - (kFirTaps - 1);  // first frame of the window for j0
+#pragma unroll
+    for (int i = 0; i < kFirTaps - 1; ++i) {
+        const int64_t f = fbase + i;  // slot (f - fbase) = i
+        w[i] = f >= 0 ? a.z[f * C + c] : a.zhist[(f + kLpfHist) * C + c];
+    }
+    float2 ys = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < kLpfJB; ++u) {
+        const int64_t j = j0 + u;
+        if (j >= a.J) break;
+        // need frames 2j and 2j+1 ; frame f lives in slot (f - fbase) mod 26
+        const int64_t f1 = 2 * j + 1;
+        const int s1 = (2 * u + kFirTaps - 1) % kFirTaps;  // slot of frame 2j+1
+        const int s0 = (2 * u + kFirTaps - 2) % kFirTaps;  // slot of frame 2j  (already loaded
+        if (u > 0) w[s0] = a.z[(f1 - 1) * C + c];           //  for u == 0 by the prologue)
+        w[s1] = a.z[f1 * C + c];
+        float yr = 0.f, yi = 0.f;
+#pragma unroll
+        for (int i = 0; i < kFirTaps; ++i) {
+            const int s = (2 * u + kFirTaps - 1 - i + kFirTaps) % kFirTaps;  // frame 2j+1-i
+            yr = fmaf(a.taps.g[i], w[s].x, yr);
+            yi = fmaf(a.taps.g[i], w[s].y, yi);
+        }
+        ys.x += yr;
+        ys.y += yi;
+        const float ph = atan2f(yi - qc, yr - ic);
+        int q = __float2int_rn(ph * 8192.0f);
+        q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
+        if (a.phase) a.phase[j * C + c] = ph;
+        a.raw[j * C + c] = (int16_t)q;
+    }
+    if (a.ysum) {
+        atomicAdd(&a.ysum[c].x, ys.x);
+        atomicAdd(&a.ysum[c].y, ys.y);
+    }
+}
+
+hipError_t launch_lpf_phase(const LpfArgs& a, hipStream_t s) {
+    if (a.J <= 0) return hipSuccess;
+    dim3 grid((unsigned)((a.J + kLpfJB - 1) / kLpfJB), (a.C + kLpfThreads - 1) / kLpfThreads);
+    hipLaunchKernelGGL(k_lpf_phase, grid, dim3(kLpfThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mkid

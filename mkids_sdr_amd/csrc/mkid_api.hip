@@ -1,0 +1,533 @@
+// C ABI of libmkidgpu.so (include/mkidgpu.h): context, configuration, streaming process calls.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mkid_internal.h"
+
+using namespace mkid;
+
+namespace {
+
+std::string g_err;
+
+// Default IQ low-pass: LUT/BlackmanFilter_250kHz.txt quantised as int(x*(2**11-1))
+// (ROACH_Pulses.py:69, 88; importFIRcoeffs default ROACH_Pulses.py:1101).
+const int16_t kBlackman250k[kFirTaps] = {0,   0,   3,   8,   17,  32,  53,  80,  111, 142, 172, 194, 206,
+                                         206, 194, 172, 142, 111, 80,  53,  32,  17,  8,   3,   0,   0};
+
+struct KTime {
+    int k;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct mkid_ctx {
+    mkid_cfg cfg{};
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    std::string err;
+    int C = 0, N = 0, M = 0, T = 0, P = 0, capc = 0;
+    int64_t Kmax = 0, Jmax = 0;
+    // configuration
+    float* d_pfb = nullptr;
+    int32_t* d_bins = nullptr;
+    float2* d_lo = nullptr;
+    int16_t* d_fir = nullptr;
+    float *d_ic = nullptr, *d_qc = nullptr;
+    int32_t* d_thr = nullptr;
+    LpfTaps lpf{};
+    int32_t mode = MKID_BASE_EMA, alpha = 41, kf = 82, kq = 93623, base_thr = 8192;
+    // stream state
+    uint32_t *d_xhist = nullptr, *d_xtmp = nullptr;
+    float2 *d_zhist = nullptr, *d_ztmp = nullptr;
+    int16_t *d_rhist = nullptr, *d_rtmp = nullptr;
+    TrigState* d_tstate = nullptr;
+    int64_t k0 = 0, j0 = 0;
+    // workspace
+    float2* d_z = nullptr;
+    int16_t* d_raw = nullptr;
+    float2* d_ysum = nullptr;
+    uint64_t* d_slots = nullptr;
+    int32_t* d_chcounts = nullptr;
+    int64_t* d_scan = nullptr;
+    int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
+    int64_t last_J = 0;
+    // host-API staging (lazy)
+    uint32_t* d_in = nullptr;
+    float* d_phase_ws = nullptr;
+    uint64_t* d_ev_ws = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<KTime> pending;
+    std::vector<hipEvent_t> pool;
+    double tot_ms[MKID_K_COUNT] = {0};
+    int64_t launches[MKID_K_COUNT] = {0};
+};
+
+#define FAIL(ctx, code, msg)       \
+    do {                           \
+        (ctx)->err = (msg);        \
+        return (code);             \
+    } while (0)
+
+#define HIPCHK(ctx, call)                                                                  \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);               \
+            return MKID_E_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+static hipEvent_t get_event(mkid_ctx* c) {
+    if (!c->pool.empty()) {
+        hipEvent_t e = c->pool.back();
+        c->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+static void tstart(mkid_ctx* c, int k, KTime* kt) {
+    kt->k = -1;
+    if (!c->timing) return;
+    kt->a = get_event(c);
+    kt->b = get_event(c);
+    if (!kt->a || !kt->b) return;
+    kt->k = k;
+    (void)hipEventRecord(kt->a, c->stream);
+}
+
+static void tstop(mkid_ctx* c, KTime* kt) {
+    if (kt->k < 0) return;
+    (void)hipEventRecord(kt->b, c->stream);
+    c->pending.push_back(*kt);
+}
+
+static int flush_timing(mkid_ctx* c) {
+    for (auto& kt : c->pending) {
+        HIPCHK(c, hipEventSynchronize(kt.b));
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, kt.a, kt.b));
+        c->tot_ms[kt.k] += ms;
+        c->launches[kt.k] += 1;
+        c->pool.push_back(kt.a);
+        c->pool.push_back(kt.b);
+    }
+    c->pending.clear();
+    return MKID_OK;
+}
+
+static void free_all(mkid_ctx* c) {
+    void* ptrs[] = {c->d_pfb,   c->d_bins,  c->d_lo,    c->d_fir,    c->d_ic,     c->d_qc,
+                    c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
+                    c->d_rtmp,  c->d_tstate, c->d_z,    c->d_raw,    c->d_ysum,   c->d_slots,
+                    c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto& kt : c->pending) {
+        (void)hipEventDestroy(kt.a);
+        (void)hipEventDestroy(kt.b);
+    }
+    for (auto e : c->pool) (void)hipEventDestroy(e);
+    if (c->own) (void)hipStreamDestroy(c->own);
+}
+
+template <typename T>
+static hipError_t dalloc(T** p, size_t n) {
+    return hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+static void default_pfb(int N, int T, std::vector<float>& h) {
+    const int L = T * N;
+    std::vector<double> d(L);
+    double s = 0;
+    for (int n = 0; n < L; ++n) {
+        const double x = (n - (L - 1) / 2.0) / N;
+        const double sinc = x == 0 ? 1.0 : std::sin(M_PI * x) / (M_PI * x);
+        d[n] = sinc * (0.54 - 0.46 * std::cos(2 * M_PI * n / (L - 1)));
+        s += d[n];
+    }
+    h.resize(L);
+    for (int n = 0; n < L; ++n) h[n] = (float)(d[n] / s);
+}
+
+extern "C" {
+
+const char* mkid_global_error(void) { return g_err.c_str(); }
+
+int mkid_default_cfg(mkid_cfg* cfg, int32_t n_channels) {
+    if (!cfg || n_channels <= 0 || 65536 % n_channels != 0) return MKID_E_ARG;
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->n_channels = n_channels;
+    cfg->fft_len = 2 * n_channels;
+    cfg->pfb_taps = kPfbTaps;
+    cfg->fir_taps = kFirTaps;
+    cfg->dds_entries = 65536 / n_channels;
+    cfg->dead_time = 32;
+    cfg->max_events_per_ch = 0;
+    cfg->max_chunk = (int64_t)1 << 22;
+    cfg->sample_rate = 512e6;
+    return MKID_OK;
+}
+
+int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
+    if (!cfg || !out) { g_err = "null argument"; return MKID_E_ARG; }
+    *out = nullptr;
+    const int C = cfg->n_channels, N = cfg->fft_len;
+    if (N != 2 * C || !channelize_supported(N)) { g_err = "unsupported geometry: need N = 2C, N in {128..4096}"; return MKID_E_ARG; }
+    if (cfg->pfb_taps != kPfbTaps || cfg->fir_taps != kFirTaps) { g_err = "pfb_taps must be 4 and fir_taps 26"; return MKID_E_ARG; }
+    const int P = cfg->dds_entries;
+    if (P <= 0 || (P & (P - 1)) != 0) { g_err = "dds_entries must be a power of two"; return MKID_E_ARG; }
+    if (cfg->max_chunk < N || cfg->max_chunk % N != 0) { g_err = "max_chunk must be a positive multiple of N"; return MKID_E_ARG; }
+    if (cfg->dead_time < 0) { g_err = "dead_time < 0"; return MKID_E_ARG; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { g_err = "no HIP device"; return MKID_E_NODEV; }
+    if (device < 0 || device >= ndev) { g_err = "bad device index"; return MKID_E_ARG; }
+    mkid_ctx* c = new (std::nothrow) mkid_ctx();
+    if (!c) { g_err = "out of host memory"; return MKID_E_ARG; }
+    c->cfg = *cfg;
+    c->device = device;
+    c->C = C; c->N = N; c->M = N / 2; c->T = kPfbTaps; c->P = P;
+    c->Kmax = cfg->max_chunk / c->M;
+    c->Jmax = cfg->max_chunk / N;
+    const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // hard bound per channel
+    c->capc = (int)std::min<int64_t>(cfg->max_events_per_ch > 0 ? cfg->max_events_per_ch : cap_bound, INT_MAX / 2);
+    const int H = c->T * N - c->M;
+    auto fail = [&](hipError_t e, const char* what) {
+        g_err = std::string(what) + ": " + hipGetErrorString(e);
+        free_all(c);
+        delete c;
+        return MKID_E_HIP;
+    };
+    hipError_t e;
+#define AL(p, n) if ((e = dalloc(&c->p, (n))) != hipSuccess) return fail(e, "hipMalloc " #p)
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail(e, "hipSetDevice");
+    if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) return fail(e, "hipStreamCreate");
+    c->stream = c->own;
+    AL(d_pfb, (size_t)c->T * N);
+    AL(d_bins, C);
+    AL(d_lo, (size_t)C * P);
+    AL(d_fir, (size_t)C * kFirTaps);
+    AL(d_ic, C);
+    AL(d_qc, C);
+    AL(d_thr, C);
+    AL(d_xhist, H);
+    AL(d_xtmp, H);
+    AL(d_zhist, (size_t)kLpfHist * C);
+    AL(d_ztmp, (size_t)kLpfHist * C);
+    AL(d_rhist, (size_t)kRawHist * C);
+    AL(d_rtmp, (size_t)kRawHist * C);
+    AL(d_tstate, C);
+    AL(d_z, (size_t)c->Kmax * C);
+    AL(d_raw, (size_t)c->Jmax * C);
+    AL(d_ysum, C);
+    AL(d_slots, (size_t)C * c->capc);
+    AL(d_chcounts, C);
+    AL(d_scan, C);
+    AL(d_counts, 2);
+#undef AL
+    // defaults: identity bins, unit LO, Blackman 250 kHz low-pass, zero matched filter (no
+    // triggers), zero centres, thresholds off, EMA baseline alpha=41 gate=8192.
+    std::vector<float> h;
+    default_pfb(N, c->T, h);
+    std::vector<int32_t> bins(C), thr(C, INT_MIN / 2);
+    for (int i = 0; i < C; ++i) bins[i] = i;
+    std::vector<float2> lo((size_t)C * P, make_float2(32767.f / 32768.f, 0.f));
+    std::vector<int16_t> fir((size_t)C * kFirTaps, 0);
+    std::vector<float> zero(C, 0.f);
+    for (int i = 0; i < kFirTaps; ++i) c->lpf.g[i] = kBlackman250k[i] / 2048.0f;
+    if ((e = hipMemcpy(c->d_pfb, h.data(), h.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_bins, bins.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_thr, thr.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_lo, lo.data(), lo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_fir, fir.data(), fir.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_ic, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_qc, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return fail(e, "hipMemcpy defaults");
+    *out = c;
+    if (mkid_reset_stream(c) != MKID_OK) {
+        g_err = c->err;
+        free_all(c);
+        delete c;
+        *out = nullptr;
+        return MKID_E_HIP;
+    }
+    return MKID_OK;
+}
+
+int mkid_destroy(mkid_ctx* c) {
+    if (!c) return MKID_E_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_all(c);
+    delete c;
+    return MKID_OK;
+}
+
+const char* mkid_last_error(const mkid_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+int mkid_get_cfg(const mkid_ctx* c, mkid_cfg* out) {
+    if (!c || !out) return MKID_E_ARG;
+    *out = c->cfg;
+    return MKID_OK;
+}
+
+int mkid_set_stream(mkid_ctx* c, void* s) {
+    if (!c) return MKID_E_ARG;
+    c->stream = s ? (hipStream_t)s : c->own;
+    return MKID_OK;
+}
+
+static int upload(mkid_ctx* c, void* dst, const void* src, size_t bytes) {
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MKID_OK;
+}
+
+int mkid_set_pfb(mkid_ctx* c, const float* coeffs, int32_t n) {
+    if (!c || !coeffs) return MKID_E_ARG;
+    if (n != c->T * c->N) FAIL(c, MKID_E_ARG, "pfb coefficient count must be T*N");
+    return upload(c, c->d_pfb, coeffs, (size_t)n * 4);
+}
+
+int mkid_set_bins(mkid_ctx* c, const int32_t* bins, int32_t n) {
+    if (!c || !bins) return MKID_E_ARG;
+    if (n != c->C) FAIL(c, MKID_E_ARG, "need one bin per channel");
+    std::vector<int32_t> b(bins, bins + n);
+    for (auto& v : b) v = ((v % c->N) + c->N) % c->N;
+    return upload(c, c->d_bins, b.data(), (size_t)n * 4);
+}
+
+int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
+    if (!c || !li || !lq) return MKID_E_ARG;
+    if (P != c->P) FAIL(c, MKID_E_ARG, "entries_per_ch must equal cfg.dds_entries");
+    std::vector<float2> lo((size_t)c->C * P);
+    for (size_t i = 0; i < lo.size(); ++i) lo[i] = make_float2(li[i] / 32768.f, -lq[i] / 32768.f);
+    return upload(c, c->d_lo, lo.data(), lo.size() * 8);
+}
+
+int mkid_set_lpf(mkid_ctx* c, const int16_t* taps, int32_t n) {
+    if (!c || !taps) return MKID_E_ARG;
+    if (n != kFirTaps) FAIL(c, MKID_E_ARG, "low-pass must have 26 taps");
+    for (int i = 0; i < n; ++i) c->lpf.g[i] = taps[i] / 2048.0f;
+    return MKID_OK;
+}
+
+int mkid_set_fir(mkid_ctx* c, const int16_t* taps, int32_t nch, int32_t nt) {
+    if (!c || !taps) return MKID_E_ARG;
+    if (nch != c->C || nt != kFirTaps) FAIL(c, MKID_E_ARG, "matched filter must be [C][26]");
+    for (int64_t i = 0; i < (int64_t)nch * nt; ++i)
+        if (taps[i] < -2048 || taps[i] > 2047) FAIL(c, MKID_E_ARG, "matched-filter tap outside 12-bit range");
+    return upload(c, c->d_fir, taps, (size_t)nch * nt * 2);
+}
+
+int mkid_set_centers(mkid_ctx* c, const float* ic, const float* qc, int32_t n) {
+    if (!c || !ic || !qc) return MKID_E_ARG;
+    if (n != c->C) FAIL(c, MKID_E_ARG, "need one centre per channel");
+    int r = upload(c, c->d_ic, ic, (size_t)n * 4);
+    return r ? r : upload(c, c->d_qc, qc, (size_t)n * 4);
+}
+
+int mkid_set_thresholds(mkid_ctx* c, const int32_t* thr, int32_t n) {
+    if (!c || !thr) return MKID_E_ARG;
+    if (n != c->C) FAIL(c, MKID_E_ARG, "need one threshold per channel");
+    return upload(c, c->d_thr, thr, (size_t)n * 4);
+}
+
+int mkid_set_baseline(mkid_ctx* c, int32_t mode, int32_t alpha, int32_t kf, int32_t kq, int32_t base_thr) {
+    if (!c) return MKID_E_ARG;
+    if (mode < MKID_BASE_NONE || mode > MKID_BASE_SVF) FAIL(c, MKID_E_ARG, "bad baseline mode");
+    if (alpha < 0 || alpha > 4095) FAIL(c, MKID_E_ARG, "alpha must be Fix12_9 (0..4095)");
+    if (kf < 0 || kf >= (1 << 18) || kq < 0 || kq >= (1 << 18)) FAIL(c, MKID_E_ARG, "kf/kq must be Fix18_16");
+    if (base_thr < 0 || base_thr > 65535) FAIL(c, MKID_E_ARG, "base_thr must be Fix16_13 (0..65535)");
+    c->mode = mode; c->alpha = alpha; c->kf = kf; c->kq = kq; c->base_thr = base_thr;
+    return MKID_OK;
+}
+
+int mkid_reset_stream(mkid_ctx* c) {
+    if (!c) return MKID_E_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int H = c->T * c->N - c->M;
+    HIPCHK(c, hipMemsetAsync(c->d_xhist, 0, (size_t)H * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_zhist, 0, (size_t)kLpfHist * c->C * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_rhist, 0, (size_t)kRawHist * c->C * 2, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_tstate, 0, (size_t)c->C * sizeof(TrigState), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 8, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->k0 = 0;
+    c->j0 = 0;
+    c->last_J = 0;
+    return MKID_OK;
+}
+
+int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
+                        int64_t cap, int64_t* d_counts) {
+    if (!c || !d_iq || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
+    if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int C = c->C, N = c->N, M = c->M;
+    const int H = c->T * N - M;
+    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 8, c->stream));
+    const uint32_t* x = (const uint32_t*)d_iq;
+    c->last_J = 0;
+    for (int64_t off = 0; off < n; off += c->cfg.max_chunk) {
+        const int64_t S = std::min<int64_t>(c->cfg.max_chunk, n - off);
+        const int64_t K = S / M, J = S / N;
+        KTime kt;
+        ChanArgs ca{x + off, c->d_xhist, c->d_pfb, c->d_bins, c->d_lo, c->d_z, K, c->k0, c->P};
+        tstart(c, MKID_K_CHANNELIZE, &kt);
+        HIPCHK(c, launch_channelize(N, ca, c->stream));
+        tstop(c, &kt);
+        HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x + off, H, S, 4, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)H * 4, hipMemcpyDeviceToDevice, c->stream));
+
+        LpfArgs la{c->d_z, c->d_zhist, c->d_ic, c->d_qc, d_phase ? d_phase + (off / N) * C : nullptr,
+                   c->d_raw, c->d_ysum, J, C, c->lpf};
+        tstart(c, MKID_K_FIR_PHASE, &kt);
+        HIPCHK(c, launch_lpf_phase(la, c->stream));
+        tstop(c, &kt);
+        HIPCHK(c, launch_hist_roll(c->d_ztmp, c->d_zhist, c->d_z, kLpfHist, K, (int64_t)C * 8, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_zhist, c->d_ztmp, (size_t)kLpfHist * C * 8, hipMemcpyDeviceToDevice, c->stream));
+
+        TrigArgs ta{c->d_raw, c->d_rhist, c->d_fir, c->d_thr, c->d_tstate, c->d_slots, c->d_chcounts,
+                    J, c->j0, C, c->capc, c->mode, c->alpha, c->kf, c->kq, c->base_thr, c->cfg.dead_time};
+        tstart(c, MKID_K_TRIGGER, &kt);
+        HIPCHK(c, launch_trigger(ta, c->stream));
+        tstop(c, &kt);
+        HIPCHK(c, launch_hist_roll(c->d_rtmp, c->d_rhist, c->d_raw, kRawHist, J, (int64_t)C * 2, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_rhist, c->d_rtmp, (size_t)kRawHist * C * 2, hipMemcpyDeviceToDevice, c->stream));
+
+        tstart(c, MKID_K_COMPACT, &kt);
+        HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, C, c->capc, d_events, cap, d_counts, c->d_scan, c->stream));
+        tstop(c, &kt);
+        c->k0 += K;
+        c->j0 += J;
+        c->last_J += J;
+    }
+    return MKID_OK;
+}
+
+int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, uint64_t* events_out, int64_t cap,
+                 int64_t* nevents) {
+    if (!c || !iq || !nevents || (cap > 0 && !events_out)) return MKID_E_ARG;
+    if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t chunk = c->cfg.max_chunk;
+    const int64_t evcap = (int64_t)c->C * c->capc;
+    if (!c->d_in) {
+        HIPCHK(c, dalloc(&c->d_in, (size_t)chunk));
+        HIPCHK(c, dalloc(&c->d_phase_ws, (size_t)c->Jmax * c->C));
+        HIPCHK(c, dalloc(&c->d_ev_ws, (size_t)evcap));
+    }
+    int64_t produced = 0, written = 0;
+    double ysx = 0, ysy = 0;
+    (void)ysx; (void)ysy;
+    for (int64_t off = 0; off < n; off += chunk) {
+        const int64_t S = std::min(chunk, n - off);
+        HIPCHK(c, hipMemcpyAsync(c->d_in, iq + 2 * off, (size_t)S * 4, hipMemcpyHostToDevice, c->stream));
+        int r = mkid_process_device(c, (const int16_t*)c->d_in, S, phase_out ? c->d_phase_ws : nullptr,
+                                    c->d_ev_ws, evcap, c->d_counts);
+        if (r) return r;
+        int64_t cnt[2];
+        HIPCHK(c, hipMemcpyAsync(cnt, c->d_counts, 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (phase_out)
+            HIPCHK(c, hipMemcpyAsync(phase_out + (off / c->N) * c->C, c->d_phase_ws,
+                                     (size_t)(S / c->N) * c->C * 4, hipMemcpyDeviceToHost, c->stream));
+        const int64_t take = std::max<int64_t>(0, std::min(cnt[1], cap - written));
+        if (take > 0)
+            HIPCHK(c, hipMemcpyAsync(events_out + written, c->d_ev_ws, (size_t)take * 8, hipMemcpyDeviceToHost,
+                                     c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        produced += cnt[0];
+        written += take;
+    }
+    *nevents = produced;
+    if (produced > written) FAIL(c, MKID_E_OVERFLOW, "event capacity exceeded; events dropped");
+    return MKID_OK;
+}
+
+int mkid_last_raw_phase(mkid_ctx* c, const int16_t** d_raw, int64_t* nrows) {
+    if (!c || !d_raw || !nrows) return MKID_E_ARG;
+    *d_raw = c->d_raw;
+    *nrows = std::min(c->last_J, c->Jmax);
+    return MKID_OK;
+}
+
+int mkid_avg_iq(mkid_ctx* c, float* mi, float* mq) {
+    if (!c || !mi || !mq) return MKID_E_ARG;
+    if (c->last_J <= 0) FAIL(c, MKID_E_STATE, "no data processed yet");
+    std::vector<float2> s(c->C);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(s.data(), c->d_ysum, (size_t)c->C * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < c->C; ++i) {
+        mi[i] = (float)(s[i].x / (double)c->last_J);
+        mq[i] = (float)(s[i].y / (double)c->last_J);
+    }
+    return MKID_OK;
+}
+
+int mkid_set_timing(mkid_ctx* c, int32_t enable) {
+    if (!c) return MKID_E_ARG;
+    int r = flush_timing(c);
+    if (r) return r;
+    c->timing = enable != 0;
+    for (int k = 0; k < MKID_K_COUNT; ++k) { c->tot_ms[k] = 0; c->launches[k] = 0; }
+    return MKID_OK;
+}
+
+int mkid_get_timing(mkid_ctx* c, int32_t k, double* total_ms, int64_t* launches) {
+    if (!c || k < 0 || k >= MKID_K_COUNT || !total_ms || !launches) return MKID_E_ARG;
+    int r = flush_timing(c);
+    if (r) return r;
+    *total_ms = c->tot_ms[k];
+    *launches = c->launches[k];
+    return MKID_OK;
+}
+
+const char* mkid_kernel_name(int32_t k) {
+    static const char* names[MKID_K_COUNT] = {"k_channelize", "k_lpf_phase", "k_trigger", "k_compact"};
+    return (k >= 0 && k < MKID_K_COUNT) ? names[k] : "?";
+}
+
+int mkid_synth_adc(mkid_ctx* c, int16_t* d_out, int64_t n, int64_t n0, const int16_t* d_base,
+                   const mkid_synth_tone* d_tones, const mkid_pulse* d_pulses, int64_t npulses, float tr,
+                   float tf, int32_t window, float sigma, uint32_t seed) {
+    if (!c || !d_out || !d_base || n < 0 || (npulses > 0 && (!d_pulses || !d_tones))) return MKID_E_ARG;
+    if (tr <= 0.f || tf <= 0.f || window < 0) FAIL(c, MKID_E_ARG, "bad pulse shape");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, launch_synth(d_out, n, n0, d_base, d_tones, d_pulses, npulses, tr, tf, window, sigma, seed,
+                           c->stream));
+    return MKID_OK;
+}
+
+int mkid_pack_reference(const uint64_t* wide, int64_t n, uint64_t* out) {
+    if ((!wide || !out) && n > 0) return MKID_E_ARG;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint64_t w = wide[i];
+        const uint64_t ch = (w >> MKID_PKT_CH_SHIFT) & 0xFFF;
+        if (ch >= 255) return MKID_E_ARG;  // 8-bit channel field, 255 = end-of-second marker
+        const uint64_t pk = (w >> MKID_PKT_PEAK_SHIFT) & 0xFFF, bs = (w >> MKID_PKT_BASE_SHIFT) & 0xFFF;
+        const uint64_t p1 = (uint64_t)std::min<int64_t>(4095, std::max<int64_t>(0, (int64_t)pk - (int64_t)bs + 2048));
+        const uint64_t ts = w & 0xFFFFF;
+        out[i] = (ch << 56) | (pk << 44) | (p1 << 32) | (bs << 20) | ts;
+    }
+    return MKID_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// Internal declarations shared by the HIP translation units of libmkidgpu.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "mkidgpu.h"
+
+namespace mkid {
+
+constexpr int kPfbTaps = 4;    // T: PFB taps per branch (build decision)
+constexpr int kFirTaps = 26;   // ROACH_Pulses.py:61
+constexpr int kLpfHist = kFirTaps - 2;  // z frames carried for the decimating IQ low-pass
+constexpr int kRawHist = kFirTaps - 1;  // raw phase samples carried for the matched filter
+
+// Per-channel trigger state. Byte layout identical to oracle/trigger.c trig_state.
+struct TrigState {
+    int32_t B, binit, st, cnt, f1, f2, pad0, pad1;
+    int64_t low, band;
+};
+static_assert(sizeof(TrigState) == 48, "TrigState layout");
+
+struct LpfTaps { float g[kFirTaps]; };
+
+struct ChanArgs {
+    const uint32_t* x;      // chunk, int16 I/Q packed per 32-bit word
+    const uint32_t* xhist;  // T*N - M previous samples
+    const float* pfb;       // T*N prototype
+    const int32_t* bins;    // C
+    const float2* lo;       // C*P, conj(LUT)/2^15
+    float2* z;              // [K][C]
+    int64_t K;              // frames in this chunk
+    int64_t k0;             // global index of the chunk's first frame
+    int32_t P;              // LO period (power of two)
+};
+
+struct LpfArgs {
+    const float2* z;        // [K][C]
+    const float2* zhist;    // [24][C]
+    const float* ic;        // C
+    const float* qc;        // C
+    float* phase;           // [J][C] or nullptr
+    int16_t* raw;           // [J][C]
+    float2* ysum;           // [C] per-channel sum of y (avgIQ) or nullptr
+    int64_t J;
+    int32_t C;
+    LpfTaps taps;
+};
+
+struct TrigArgs {
+    const int16_t* raw;     // [J][C]
+    const int16_t* rhist;   // [25][C]
+    const int16_t* fir;     // [C][26]
+    const int32_t* thr;     // [C]
+    TrigState* st;          // [C]
+    uint64_t* slots;        // [C][capc]
+    int32_t* counts;        // [C]
+    int64_t J;
+    int64_t j0;             // global index of the chunk's first phase sample
+    int32_t C;
+    int32_t capc;
+    int32_t mode, alpha, kf, kq, base_thr, dead;
+};
+
+// launchers (return hipError_t of the launch)
+hipError_t launch_channelize(int N, const ChanArgs& a, hipStream_t s);
+hipError_t launch_lpf_phase(const LpfArgs& a, hipStream_t s);
+hipError_t launch_trigger(const TrigArgs& a, hipStream_t s);
+hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int32_t C, int32_t capc,
+                          uint64_t* out, int64_t cap, int64_t* d_counts, int64_t* scan_ws,
+                          hipStream_t s);
+hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
+                            int64_t fresh_rows, int64_t row_bytes, hipStream_t s);
+hipError_t launch_synth(int16_t* out, int64_t n, int64_t n0, const int16_t* base,
+                        const mkid_synth_tone* tones, const mkid_pulse* pulses, int64_t npulses,
+                        float tr, float tf, int32_t window, float sigma, uint32_t seed,
+                        hipStream_t s);
+
+bool channelize_supported(int N);
+
+}  // namespace mkid

@@ -1,0 +1,181 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on identical seeded inputs.
+
+Bars: phase within 1e-5 rad of the float64 oracle on every tone channel;
+Fix16_13 phase within 1 LSB (rounding-boundary flips only, rare); photon packets bit-exact —
+both the full chain vs the oracle chain, and the device trigger vs the oracle trigger fed the
+device's own Fix16_13 phase.
+"""
+import numpy as np
+import pytest
+
+import signals
+from oracle import trigger as otrig
+
+pytestmark = pytest.mark.gpu
+
+PHASE_TOL = 1e-5
+
+
+def configure(ch, case, thr, mode=1):
+    ch.set_pfb(case.pfb)
+    ch.set_bins(case.bins)
+    ch.set_dds(case.lut_i, case.lut_q)
+    ch.set_lpf(case.lpf12)
+    ch.set_fir(case.fir12)
+    ch.set_centers(case.ic, case.qc)
+    ch.set_thresholds(thr)
+    ch.set_baseline(mode, 41, 82, 93623, 8192)
+
+
+def quiet_thresholds(C, S, seed):
+    q = signals.make_case(C, S, seed=seed, pulses_per_ch=0)
+    r = signals.oracle_chain(q).process(q.iq)
+    return signals.thresholds_from_quiet(q, r['raw'])
+
+
+def sort_events(ev):
+    ev = np.asarray(ev, np.uint64)
+    key = (ev >> np.uint64(52)) * np.uint64(1 << 28) + (ev & np.uint64((1 << 28) - 1))
+    return ev[np.argsort(key, kind='stable')]
+
+
+def split_by_channel(ev):
+    out = {}
+    for w in sort_events(ev):
+        out.setdefault(int(w) >> 52, []).append(int(w))
+    return out
+
+
+def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32):
+    from mkids_sdr_amd.channelizer import Channelizer
+    S = case.iq.shape[0]
+    ch = Channelizer(case.C, max_chunk=max_chunk or S, dead_time=dead)
+    try:
+        configure(ch, case, thr, mode)
+        phases, evs = [], []
+        for a, b in zip(splits[:-1], splits[1:]):
+            ph, ev = ch.process(case.iq[a:b])
+            phases.append(ph)
+            evs.append(ev)
+        mi, mq = ch.avg_iq()
+    finally:
+        ch.close()
+    return np.concatenate(phases), np.concatenate(evs), (mi, mq)
+
+
+def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=True):
+    o = signals.oracle_chain(case)
+    r = o.process(case.iq)
+    tr = otrig.Trigger(case.C, case.fir12, thr, mode=mode, dead=dead)
+    ev_o, n_o, _ = tr.run(r['raw'])
+    ph_g, ev_g, _ = run_gpu(case, thr, splits, mode, max_chunk, dead)
+
+    assert ph_g.shape == r['phase'].shape
+    tones = slice(0, case.n_tones)
+    err = np.abs(signals.wrap(ph_g[:, tones].astype(np.float64) - r['phase'][:, tones]))
+    assert err.max() < PHASE_TOL, 'phase error %.3g rad' % err.max()
+
+    raw_g = np.clip(np.rint(ph_g * np.float32(8192)), -25736, 25736).astype(np.int64)
+    draw = np.abs(raw_g[:, tones] - r['raw'][:, tones].astype(np.int64))
+    assert draw.max() <= 1
+    assert (draw > 0).mean() < 1e-3
+
+    # device trigger == oracle trigger on the device's own Fix16_13 phase (exact integer path)
+    tr2 = otrig.Trigger(case.C, case.fir12, thr, mode=mode, dead=dead)
+    ev_same, _, _ = tr2.run(raw_g.astype(np.int16))
+    assert np.array_equal(sort_events(ev_g), sort_events(ev_same))
+    # full chain: GPU packets == oracle-chain packets, channel by channel. The only admissible
+    # difference is downstream of a Fix16_13 rounding-boundary flip (fp32 vs float64 phase that
+    # straddles a half-LSB): a channel may differ only at or after its first flipped sample.
+    g_by, o_by = split_by_channel(ev_g), split_by_channel(ev_o)
+    n_diff_ch = 0
+    for c in range(case.C):
+        a, b = g_by.get(c, []), o_by.get(c, [])
+        if a == b:
+            continue
+        n_diff_ch += 1
+        flips = np.nonzero(raw_g[:, c] != r['raw'][:, c].astype(np.int64))[0]
+        assert flips.size, 'channel %d packets differ with identical Fix16_13 phase' % c
+        first_diff = next(i for i in range(min(len(a), len(b)) + 1)
+                          if i >= len(a) or i >= len(b) or a[i] != b[i])
+        t_diff = min([(w & ((1 << 28) - 1)) for w in (a[first_diff:first_diff + 1] +
+                                                     b[first_diff:first_diff + 1])])
+        assert t_diff + 1 >= flips[0], 'channel %d differs before its first phase flip' % c
+    assert n_diff_ch <= max(1, case.C // 200)
+    if expect_events:
+        assert n_o > 0
+    return ph_g, ev_g, r
+
+
+@pytest.mark.parametrize('C,S,splits,seed', [
+    (64, 2 ** 16, None, 1),                       # config 1 geometry (64 ch, 2^16 samples)
+    (128, 2 ** 17, [0, 2 ** 15, 2 ** 17], 2),
+    (256, 2 ** 18, [0, 2 ** 16 + 512, 2 ** 17, 2 ** 18], 3),   # config 2 geometry, streamed
+    (512, 2 ** 18, None, 4),
+    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5),    # config 3 geometry
+    (2048, 2 ** 20, None, 6),                     # config 5 geometry
+])
+def test_chain_parity(gpu, C, S, splits, seed):
+    case = signals.make_case(C, S, seed=seed, pulses_per_ch=max(1.0, S / (2 * C) / 400))
+    thr = quiet_thresholds(C, min(S, 2 * C * 2048), seed)
+    compare(case, thr, splits or [0, S])
+
+
+@pytest.mark.parametrize('mode', [0, 1, 2])
+def test_baseline_modes(gpu, mode):
+    C, S = 256, 2 ** 18
+    case = signals.make_case(C, S, seed=11, pulses_per_ch=2.0)
+    thr = quiet_thresholds(C, S, 11)
+    if mode == 0:  # absolute threshold: below the tone's mean filtered phase
+        o = signals.oracle_chain(case)
+        raw = o.process(case.iq)['raw'].astype(np.int64)
+        thr = (np.median(raw, axis=0) * 1.38 - 1500).astype(np.int64)
+    compare(case, thr, [0, 2 ** 17, S], mode=mode)
+
+
+def test_internal_subchunks_and_tiny_calls(gpu):
+    """max_chunk < call size (internal sub-chunking) and calls of exactly N samples."""
+    C, S = 64, 2 ** 15
+    case = signals.make_case(C, S, seed=21, pulses_per_ch=2.0)
+    thr = quiet_thresholds(C, S, 21)
+    compare(case, thr, [0, S], max_chunk=8 * 2 * C)
+    splits = list(range(0, 40 * 2 * C, 2 * C)) + [S]
+    compare(case, thr, splits)
+
+
+def test_deleted_channels_and_dead_time(gpu):
+    C, S = 128, 2 ** 17
+    case = signals.make_case(C, S, seed=31, pulses_per_ch=3.0)
+    thr = quiet_thresholds(C, S, 31)
+    case.fir12[::2] = 0  # zero taps delete a channel (ROACH_Pulses.py:64-67)
+    _, ev, _ = compare(case, thr, [0, S], dead=0)
+    chans = (np.asarray(ev, np.uint64) >> np.uint64(52)).astype(np.int64)
+    assert np.all(chans % 2 == 1)
+    compare(case, thr, [0, S], dead=200)
+
+
+def test_avg_iq_matches_oracle(gpu):
+    C, S = 256, 2 ** 17
+    case = signals.make_case(C, S, seed=41)
+    thr = np.full(C, -(1 << 30))
+    _, _, (mi, mq) = run_gpu(case, thr, [0, S])
+    y = signals.oracle_chain(case).process(case.iq)['y']
+    np.testing.assert_allclose(mi, y.real.mean(0), rtol=1e-4, atol=1e-2)
+    np.testing.assert_allclose(mq, y.imag.mean(0), rtol=1e-4, atol=1e-2)
+
+
+def test_errors_are_loud(gpu):
+    from mkids_sdr_amd import _lib
+    from mkids_sdr_amd.channelizer import Channelizer
+    ch = Channelizer(64)
+    try:
+        with pytest.raises(_lib.MkidError):
+            ch.process(np.zeros((100, 2), np.int16))          # not a multiple of N
+        with pytest.raises(_lib.MkidError):
+            ch.set_fir(np.full((64, 26), 5000, np.int16))     # outside 12-bit
+        with pytest.raises(_lib.MkidError):
+            ch.set_bins(np.zeros(3, np.int32))                # wrong length
+    finally:
+        ch.close()
+    with pytest.raises(_lib.MkidError):
+        Channelizer(100)                                      # N = 200 unsupported

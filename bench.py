@@ -61,7 +61,8 @@ def setup_feedline(C, fs, seed):
     base = np.stack([I_dac, -Q_dac], axis=1).astype(np.int16)       # loop-back conjugation
     freq_index = np.array([int(round(((fs - f) % fs) / res)) for f in freqs_dac], np.int64)
     tone_amp = lut.FULL_SCALE / sf
-    return dict(dds=dds, base=base, freq_index=freq_index, phases=phases, tone_amp=tone_amp)
+    return dict(dds=dds, base=base, freq_index=freq_index, phases=phases, tone_amp=tone_amp,
+                f_rf=f_rf, f_base=f_base)
 
 
 def make_pulses(C, n_samples, N, rate, rng, tau_fall=65.0, window_phase=390):
@@ -131,7 +132,9 @@ def main():
     sigma = 0.01 * 32767 / np.sqrt(2.0)
     ch.synth_adc(x, S, 0, base, d_tones, d_pul, len(ps), 0.1 * N, 65.0 * N, 390 * N, sigma, 42 + rank)
 
-    # ---- thresholds the reference way (loadThresholds on a pulse-free phase snapshot) ----
+    # ---- loop calibration + thresholds the reference way, on a pulse-free stream:
+    #      rotateLoopsReady (ROACH_Setup.py:645-667: DDS phase = arctan2 of the on-resonance avg
+    #      IQ, so every channel's phase sits near 0), then loadThresholds (ROACH_Pulses.py:211-299)
     quiet_n = 1 << 24
     q = torch.empty(quiet_n * 2, dtype=torch.int16, device=dev)
     ch.synth_adc(q, quiet_n, 0, base, d_tones, d_pul, 0, 0.1 * N, 65.0 * N, 390 * N, sigma, 7 + rank)
@@ -140,6 +143,13 @@ def main():
     d_events = torch.empty(cap, dtype=torch.int64, device=dev)
     d_counts = torch.zeros(2, dtype=torch.int64, device=dev)
     ch.set_thresholds(np.full(C, -(1 << 30), np.int32))
+    ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
+    torch.cuda.synchronize(dev)
+    mi, mq = ch.avg_iq()
+    from mkids_sdr_amd import lut as _lut
+    feed['dds'] = _lut.define_dds_lut(feed['f_rf'], feed['f_base'], C, fs, phase=np.arctan2(mq, mi))
+    ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
+    ch.reset()
     ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
     torch.cuda.synchronize(dev)
     raw_q = torch.clamp(torch.round(qphase * 8192), -25736, 25736).view(-1, C).cpu().numpy().astype(np.int64)
@@ -184,6 +194,7 @@ def main():
     timing = ch.timing()
     counts = d_counts.cpu().numpy()
     ev_last = int(counts[0])
+    reruns = ch.trigger_reruns()
 
     if rank == 0:
         total = S * args.steps * world
@@ -227,6 +238,8 @@ def main():
                        'parallelism': 'feedline-per-GPU x%d, RCCL packet gather' % world},
             'per_gpu_msps': round(value / world, 1),
             'packets_per_step_rank0': ev_last,
+            'injected_pulses_rank0': int(len(ps)),
+            'trigger_segments_rerun': reruns,
             'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1),
                          'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBPS, 4), 'traffic': traffic,

@@ -137,6 +137,10 @@ int mkid_process_device(mkid_ctx* ctx, const int16_t* d_iq, int64_t nsamples, fl
  * (ROACH_Pulses.py:357-378). */
 int mkid_last_raw_phase(mkid_ctx* ctx, const int16_t** d_raw, int64_t* nrows);
 
+/* Diagnostic: trigger segments of the last sub-chunk whose speculative start state had to be
+ * re-run by the exact fix-up pass (0 = all speculation was right; results are exact either way). */
+int mkid_trigger_reruns(mkid_ctx* ctx, int64_t* total);
+
 /* Per-channel mean I/Q of the last processed call (avgIQ_bram, ROACH_Setup.py:654-662), [C] each. */
 int mkid_avg_iq(mkid_ctx* ctx, float* mean_i, float* mean_q);
 

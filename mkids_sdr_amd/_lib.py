@@ -71,6 +71,7 @@ _SIGS = {
     'mkid_process_device': [P, P, I64, P, P, I64, P],
     'mkid_last_raw_phase': [P, P, P],
     'mkid_avg_iq': [P, P, P],
+    'mkid_trigger_reruns': [P, P],
     'mkid_pack_reference': [P, I64, P],
     'mkid_set_timing': [P, I32],
     'mkid_get_timing': [P, I32, P, P],

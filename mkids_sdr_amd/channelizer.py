@@ -124,6 +124,11 @@ class Channelizer:
         self._chk(self._L.mkid_last_raw_phase(self._h, ctypes.byref(p), ctypes.byref(n)))
         return p.value, n.value
 
+    def trigger_reruns(self):
+        n = ctypes.c_int64()
+        self._chk(self._L.mkid_trigger_reruns(self._h, ctypes.byref(n)))
+        return n.value
+
     def avg_iq(self):
         mi = np.empty(self.C, np.float32)
         mq = np.empty(self.C, np.float32)

@@ -1,10 +1,14 @@
 // K1-K4: polyphase filter bank + N-point FFT (2x oversampled, hop M = N/2) + bin select + DDC.
 //
-// One 256-thread workgroup owns FPB = 256/NT frame slots (NT = N/PTS threads per frame, PTS
-// points per thread) and walks FL consecutive frame groups. Per frame:
-//   PFB   u[p] = sum_tau h[tau N + p] x[(k+1)M - TN + tau N + p]     (p = t + r NT: coalesced)
-//   FFT   Stockham radix-16/8/4 passes, butterflies in registers, exchanges through padded LDS
-//   K3/4  z[k][c] = X[bin_c] * (-1)^(bin_c (k+1)) * conj(LUT_c[k mod P]) / 2^15
+// A workgroup of BT threads owns a contiguous run of frames and walks it FPB frames at a time
+// (NT = N/PTS threads per frame, PTS = 8 points per thread, FPB = BT/NT):
+//   input  ring of RS = 2T-1+FPB hops of M int16 I/Q samples in LDS. Each iteration brings FPB
+//          new hops with ONE 16-byte global load per thread, issued one iteration ahead so its
+//          latency hides behind the FFT; each sample is read from HBM once (+ (2T-1)/run warm-up).
+//   PFB    u[p] = sum_tau h[tau N + p] x[(k+1)M - TN + tau N + p]  (h in registers, x from LDS)
+//   FFT    Stockham radix-8/4 passes, butterflies in registers, twiddles in registers, exchanges
+//          through padded LDS
+//   K3/4   z[k][c] = X[bin_c] (-1)^(bin_c (k+1)) conj(LUT_c[k mod P]) / 2^15, coalesced stores
 // Reference geometry: fft_len/channels ROACH_Setup.py:507,515; bins ROACH_Setup.py:534-550; DDS
 // LUT at 2 fs/N ROACH_Setup.py:525. Taps/window of the PFB: build decision (firmware absent).
 #include "fft_common.h"
@@ -12,87 +16,162 @@
 
 namespace mkid {
 
-constexpr int kChanThreads = 256;
-constexpr int kFramesPerIter = 8;  // FL
+template <int N>
+struct Plan8;  // PTS = 8 points per thread; radix sequence R1..R4 (1 = no pass)
+template <> struct Plan8<128>  { static constexpr int NP = 3, R[4] = {8, 4, 4, 1}; };
+template <> struct Plan8<256>  { static constexpr int NP = 3, R[4] = {8, 8, 4, 1}; };
+template <> struct Plan8<512>  { static constexpr int NP = 3, R[4] = {8, 8, 8, 1}; };
+template <> struct Plan8<1024> { static constexpr int NP = 4, R[4] = {8, 8, 4, 4}; };
+template <> struct Plan8<2048> { static constexpr int NP = 4, R[4] = {8, 8, 8, 4}; };
+template <> struct Plan8<4096> { static constexpr int NP = 4, R[4] = {8, 8, 8, 8}; };
+
+constexpr int kPts = 8;
 
 template <int N>
-__global__ __launch_bounds__(kChanThreads) void k_channelize(ChanArgs a) {
-    using PL = Plan<N>;
-    constexpr int PTS = PL::PTS, NT = N / PTS, FPB = kChanThreads / NT;
-    constexpr int M = N / 2, C = N / 2, T = kPfbTaps, H = T * N - M;
-    constexpr int LDSF = lds_frame_elems<N>();
-    constexpr int CPT = C / NT;  // channels per thread in the select stage
-    __shared__ float2 lds[FPB * LDSF];
+struct Geo {
+    static constexpr int PTS = kPts, NT = N / PTS;
+    static constexpr int BT = NT > 256 ? NT : 256;     // threads per workgroup
+    static constexpr int FPB = BT / NT;                 // frames in flight per workgroup
+    static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
+    static constexpr int RS = 2 * T - 1 + FPB;          // ring slots (hops)
+    static constexpr int LDSF = lds_frame_elems<N>();
+    static constexpr int CPT = C / NT;                  // channels per thread in select
+    static constexpr int NEW = FPB * M;                 // new samples per iteration
+    static constexpr int SPT = NEW / BT;                // new samples per thread (4)
+    static_assert(SPT == 4, "one 16-byte load per thread per iteration");
+    static constexpr int NS2 = Plan8<N>::R[0], NS3 = NS2 * Plan8<N>::R[1], NS4 = NS3 * Plan8<N>::R[2];
+    static constexpr size_t lds_bytes = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8;
+};
 
-    const int slot = threadIdx.x / NT;
-    const int t = threadIdx.x % NT;
-    float2* buf = lds + slot * LDSF;
+// Load the 16 bytes (4 samples) this thread contributes to hop-group `it` of the run.
+template <int N>
+__device__ __forceinline__ uint4 load_new(const ChanArgs& a, int64_t first_hop, int tid) {
+    using G = Geo<N>;
+    const int64_t s0 = first_hop * G::M + (int64_t)tid * G::SPT;  // sample index in chunk
+    if (s0 >= (int64_t)a.K * G::M) return make_uint4(0, 0, 0, 0);
+    if (s0 >= 0) return *reinterpret_cast<const uint4*>(a.x + s0);
+    const int64_t hs = s0 + (G::T * N - G::M);  // into xhist (H = TN - M samples)
+    return *reinterpret_cast<const uint4*>(a.xhist + hs);
+}
 
-    Twiddle<N, PTS, PL::R2, PL::R1> tw2;
-    tw2.init(t);
-    Twiddle<N, PTS, (PL::NP == 3 ? PL::R3 : 2), PL::R1 * PL::R2> tw3;
-    if constexpr (PL::NP == 3) tw3.init(t);
+template <int N>
+__global__ __launch_bounds__(Geo<N>::BT) void k_channelize(ChanArgs a) {
+    using G = Geo<N>;
+    using PL = Plan8<N>;
+    constexpr int PTS = G::PTS, NT = G::NT, M = G::M, C = G::C, T = G::T, RS = G::RS;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
+    float2* fbuf = reinterpret_cast<float2*>(smem + (size_t)RS * M * 4);
 
-    int32_t bin[CPT];
+    const int tid = threadIdx.x;
+    const int slot = tid / NT;
+    const int t = tid % NT;
+    float2* buf = fbuf + slot * G::LDSF;
+
+    // PFB taps for this thread's points (constant over frames)
+    float h[T][PTS];
 #pragma unroll
-    for (int q = 0; q < CPT; ++q) bin[q] = a.bins[t + q * NT];
+    for (int tau = 0; tau < T; ++tau)
+#pragma unroll
+        for (int r = 0; r < PTS; ++r) h[tau][r] = a.pfb[tau * N + t + r * NT];
 
-    const int64_t kbase = (int64_t)blockIdx.x * FPB * kFramesPerIter;
-    for (int it = 0; it < kFramesPerIter; ++it) {
-        const int64_t k = kbase + (int64_t)it * FPB + slot;
-        const bool valid = k < a.K;
-        const int64_t kk = valid ? k : a.K - 1;
+    Twiddle<N, PTS, PL::R[1], G::NS2> tw2;
+    tw2.init(t);
+    Twiddle<N, PTS, PL::R[2], G::NS3> tw3;
+    tw3.init(t);
+    Twiddle<N, PTS, (PL::NP == 4 ? PL::R[3] : 2), G::NS4> tw4;
+    if constexpr (PL::NP == 4) tw4.init(t);
 
-        // ---- PFB ----
+    int32_t bin[G::CPT];
+#pragma unroll
+    for (int q = 0; q < G::CPT; ++q) bin[q] = a.bins[t + q * NT];
+
+    const int64_t k_begin = (int64_t)blockIdx.x * a.frames_per_block;
+    int64_t k_end = k_begin + a.frames_per_block;
+    if (k_end > a.K) k_end = a.K;
+    if (k_begin >= k_end) return;
+
+    // prologue: hops k_begin-2T+1 .. k_begin+FPB-1 -> ring (slot = hop mod RS)
+    {
+        const int64_t h0 = k_begin - 2 * T + 1;
+        for (int g = 0; g < RS; g += G::FPB) {
+            const int64_t hop = h0 + g + (tid * G::SPT) / M;
+            if (hop > h0 + RS - 1) continue;  // RS need not be a multiple of FPB
+            const uint4 v = load_new<N>(a, h0 + g, tid);
+            const int off = (tid * G::SPT) % M;
+            *reinterpret_cast<uint4*>(ring + (int)(((hop % RS) + RS) % RS) * M + off) = v;
+        }
+    }
+    uint4 pre = load_new<N>(a, k_begin + G::FPB, tid);  // next iteration's hops
+    __syncthreads();
+
+    for (int64_t kb = k_begin; kb < k_end; kb += G::FPB) {
+        const int64_t k = kb + slot;  // this thread's frame
+        // ---- PFB from the LDS ring ----
+        const int64_t h_first = k + 1 - 2 * T;  // oldest hop of frame k
+        const int sb = (int)(((h_first % RS) + RS) % RS);
         float2 v[PTS];
-        const int64_t n0 = (kk + 1) * M - (int64_t)T * N;
 #pragma unroll
         for (int r = 0; r < PTS; ++r) {
             const int p = t + r * NT;
+            const int hi = p / M, off = p % M;
             float ur = 0.f, ui = 0.f;
 #pragma unroll
             for (int tau = 0; tau < T; ++tau) {
-                const int64_t n = n0 + tau * N + p;
-                const uint32_t w = n >= 0 ? a.x[n] : a.xhist[n + H];
-                const float h = a.pfb[tau * N + p];
-                ur = fmaf(h, (float)(int16_t)(w & 0xffffu), ur);
-                ui = fmaf(h, (float)(int16_t)(w >> 16), ui);
+                int sl = sb + 2 * tau + hi;  // < 2 RS
+                sl -= sl >= RS ? RS : 0;
+                const uint32_t w = ring[sl * M + off];
+                ur = fmaf(h[tau][r], (float)(int16_t)(w & 0xffffu), ur);
+                ui = fmaf(h[tau][r], (float)(int16_t)(w >> 16), ui);
             }
             v[r] = make_float2(ur, ui);
         }
-
+        st_dft<PTS, PL::R[0]>(v);
+        __syncthreads();  // all PFB reads of the oldest FPB hops are done
+        {   // refill the ring with the prefetched hops, start the next prefetch
+            const int64_t hop = kb + G::FPB + (tid * G::SPT) / M;
+            const int off = (tid * G::SPT) % M;
+            *reinterpret_cast<uint4*>(ring + (int)(hop % RS) * M + off) = pre;
+            pre = load_new<N>(a, kb + 2 * G::FPB, tid);
+        }
         // ---- FFT ----
-        st_dft<PTS, PL::R1>(v);
-        st_write<N, PTS, PL::R1, 1>(buf, v, t);
+        st_write<N, PTS, PL::R[0], 1>(buf, v, t);
         __syncthreads();
-        st_read<N, PTS, PL::R2>(buf, v, t);
+        st_read<N, PTS, PL::R[1]>(buf, v, t);
         __syncthreads();
         tw2.apply(v);
-        st_dft<PTS, PL::R2>(v);
-        st_write<N, PTS, PL::R2, PL::R1>(buf, v, t);
+        st_dft<PTS, PL::R[1]>(v);
+        st_write<N, PTS, PL::R[1], G::NS2>(buf, v, t);
         __syncthreads();
-        if constexpr (PL::NP == 3) {
-            st_read<N, PTS, PL::R3>(buf, v, t);
+        st_read<N, PTS, PL::R[2]>(buf, v, t);
+        __syncthreads();
+        tw3.apply(v);
+        st_dft<PTS, PL::R[2]>(v);
+        st_write<N, PTS, PL::R[2], G::NS3>(buf, v, t);
+        __syncthreads();
+        if constexpr (PL::NP == 4) {
+            st_read<N, PTS, PL::R[3]>(buf, v, t);
             __syncthreads();
-            tw3.apply(v);
-            st_dft<PTS, PL::R3>(v);
-            st_write<N, PTS, PL::R3, PL::R1 * PL::R2>(buf, v, t);
+            tw4.apply(v);
+            st_dft<PTS, PL::R[3]>(v);
+            st_write<N, PTS, PL::R[3], G::NS4>(buf, v, t);
             __syncthreads();
         }
-
         // ---- bin select + DDC ----
-        const int64_t kg = a.k0 + kk;
-        const int podd = (int)((kg + 1) & 1);
-        const int lidx = (int)(kg & (a.P - 1));
+        if (k < k_end) {
+            const int64_t kg = a.k0 + k;
+            const int podd = (int)((kg + 1) & 1);
+            const int lidx = (int)(kg & (a.P - 1));
 #pragma unroll
-        for (int q = 0; q < CPT; ++q) {
-            const int c = t + q * NT;
-            float2 X = buf[lpad(bin[q])];
-            if (podd & bin[q] & 1) X = make_float2(-X.x, -X.y);
-            const float2 lo = a.lo[(int64_t)c * a.P + lidx];
-            if (valid) a.z[kk * C + c] = cmul(X, lo);
+            for (int q = 0; q < G::CPT; ++q) {
+                const int c = t + q * NT;
+                float2 X = buf[lpad(bin[q])];
+                if (podd & bin[q] & 1) X = make_float2(-X.x, -X.y);
+                const float2 lo = a.lo[(int64_t)c * a.P + lidx];
+                a.z[k * C + c] = cmul(X, lo);
+            }
         }
-        __syncthreads();
+        // the next iteration's first LDS write (ring refill) happens after its own barrier
     }
 }
 
@@ -101,12 +180,26 @@ bool channelize_supported(int N) {
 }
 
 template <int N>
-static hipError_t launch_n(const ChanArgs& a, hipStream_t s) {
-    constexpr int NT = N / Plan<N>::PTS, FPB = kChanThreads / NT;
-    const int64_t per_block = (int64_t)FPB * kFramesPerIter;
-    const int64_t blocks = (a.K + per_block - 1) / per_block;
-    if (blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_channelize<N>, dim3((unsigned)blocks), dim3(kChanThreads), 0, s, a);
+static hipError_t launch_n(const ChanArgs& a0, hipStream_t s) {
+    using G = Geo<N>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_channelize<N>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)G::lds_bytes);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    ChanArgs a = a0;
+    if (a.K <= 0) return hipSuccess;
+    // contiguous frame runs: long enough to amortise the (2T-1)-hop warm-up, enough runs to
+    // give every CU several workgroups
+    int64_t fpb = a.K / 2048;
+    fpb = fpb < 64 ? 64 : (fpb > 1024 ? 1024 : fpb);
+    fpb = (fpb + G::FPB - 1) / G::FPB * G::FPB;
+    a.frames_per_block = fpb;
+    const int64_t blocks = (a.K + fpb - 1) / fpb;
+    hipLaunchKernelGGL(k_channelize<N>, dim3((unsigned)blocks), dim3(G::BT), G::lds_bytes, s, a);
     return hipGetLastError();
 }
 

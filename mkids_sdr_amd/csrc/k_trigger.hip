@@ -1,124 +1,180 @@
 // K7-K8: matched filter + baseline (EMA / SVF) + threshold + parabolic peak + dead time +
-// packetiser, and the deterministic channel-major compaction of the per-channel event slots.
-// Integer semantics are bit-identical to oracle/trigger.c (the oracle header lists the reference
-// anchors: ROACH_Pulses.py:59-111, 211-299; set_alpha.py; set_svf.py; set_base_thresh.py;
-// Utils/bin.py:5-16; packet fields ROACH_Pulses.py:796-859).
-#include "mkid_internal.h"
+// packetiser, evaluated EXACTLY but in parallel over time by speculative segments:
+//
+//   k_trig_spec  thread = (channel c, segment s of L phase samples). Segment 0 starts from the
+//                channel's carried state (exact). Segment s>0 starts W samples early from a guessed
+//                state (re-arm pending, baseline = first filtered sample), runs the warm-up
+//                silently, records its state S_spec at the segment start, then emits packets.
+//   k_trig_fix   thread = channel. Walks the segments in order with the true state T. If
+//                T == S_spec (canonical compare) the segment's packets are exact. Otherwise it
+//                re-runs the true and the speculative trajectories side by side from the segment
+//                start until they coincide (the recurrence is deterministic in (state, input)), and
+//                splices: true packets before the merge + speculative packets after it.
+//   compaction   exclusive scan over (channel, segment) counts -> channel-major, time-ascending.
+//
+// The result is bit-identical to the sequential oracle/trigger.c for every input; the speculation
+// only decides how much sequential work the fix-up does (EMA merges within ~10^2 samples on noisy
+// phase). SVF mode (slow 2-pole baseline with a wide dead band) uses one segment = serial.
+#include "trig_common.h"
 
 namespace mkid {
 
 constexpr int kTrigThreads = 64;
 
-__device__ __forceinline__ int32_t clamp16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
-__device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+struct Win {
+    int32_t w[kFirTaps];
+};
 
-__device__ __forceinline__ int64_t peakfit_i(int64_t y1, int64_t y2, int64_t y3) {
-    const int64_t den = y3 + y1 - 2 * y2;
-    if (den == 0) return y2;
-    const int64_t d = y3 - y1;
-    return y2 - (d * d) / (8 * den);
+// Prologue: load raw_{j-25..j-1} into ring slots (j' - j + 26) % 26 for a ring aligned at j.
+__device__ __forceinline__ void load_window(Win& win, const TrigSpecArgs& a, int c, int64_t j) {
+    win.w[0] = 0;
+#pragma unroll
+    for (int i = 1; i < kFirTaps; ++i) {
+        const int64_t jj = j - kFirTaps + i;  // slot i holds raw_{j-26+i}
+        win.w[i] = jj >= 0 ? a.raw[jj * a.C + c] : (jj >= -kRawHist ? a.rhist[(jj + kRawHist) * a.C + c] : 0);
+    }
 }
 
-__device__ __forceinline__ uint64_t pack_wide(int32_t ch, int64_t peak, int32_t base, int64_t j) {
-    const uint64_t pk = (uint64_t)clampi((int32_t)((peak >> 4) + 2048), 0, 4095);
-    const uint64_t bs = (uint64_t)clampi((base >> 4) + 2048, 0, 4095);
-    return ((uint64_t)(ch & 0xFFF) << MKID_PKT_CH_SHIFT) | (pk << MKID_PKT_PEAK_SHIFT) |
-           (bs << MKID_PKT_BASE_SHIFT) | ((uint64_t)j & MKID_PKT_TS_MASK);
+__global__ __launch_bounds__(kTrigThreads) void k_trig_spec(TrigSpecArgs a) {
+    const int c = blockIdx.x * kTrigThreads + threadIdx.x;
+    const int s = blockIdx.y;
+    if (c >= a.C) return;
+    const int C = a.C;
+    int32_t tap[kFirTaps];
+#pragma unroll
+    for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
+    const TrigCfg k{a.thr[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
+    const int64_t seg0 = (int64_t)s * a.L;
+    const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
+    const int64_t jw = s == 0 ? 0 : seg0 - a.W;
+    TrigState st;
+    if (s == 0) {
+        st = a.st_in[c];
+    } else {
+        st = TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
+    }
+    Win win;
+    load_window(win, a, c, jw);
+    const int64_t sc = (int64_t)c * a.nseg + s;
+    uint64_t* slot = a.slots + sc * a.capseg;
+    int32_t n = 0;
+    for (int64_t g = jw; g < seg1; g += kFirTaps) {
+        const int64_t left = seg1 - g;
+#pragma unroll
+        for (int u = 0; u < kFirTaps; ++u) {
+            if (u >= left) continue;
+            const int64_t j = g + u;
+            win.w[u] = a.raw[j * C + c];
+            int32_t acc = 0;
+#pragma unroll
+            for (int i = 0; i < kFirTaps; ++i) acc += tap[i] * win.w[(u - i + kFirTaps) % kFirTaps];
+            if (s > 0 && j == seg0) a.s_spec[(int64_t)s * C + c] = st;
+            uint64_t pkt;
+            if (trig_step(st, mf_out(acc), k, c, a.j0 + j, &pkt) && j >= seg0) {
+                if (n < a.capseg) slot[n] = pkt;
+                ++n;
+            }
+        }
+    }
+    a.s_end[(int64_t)s * C + c] = st;
+    a.counts[sc] = n;
 }
 
-enum { ST_ARMED = 0, ST_PULSE = 1, ST_DEAD = 2, ST_REARM = 3 };
-
-// One thread per channel, sequential in time (v1). The 26-sample matched-filter window is a
-// register ring indexed statically inside 26-sample unrolled groups.
-__global__ __launch_bounds__(kTrigThreads) void k_trigger(TrigArgs a) {
+__global__ __launch_bounds__(kTrigThreads) void k_trig_fix(TrigSpecArgs a) {
     const int c = blockIdx.x * kTrigThreads + threadIdx.x;
     if (c >= a.C) return;
     const int C = a.C;
     int32_t tap[kFirTaps];
 #pragma unroll
     for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
-    const int32_t thr = a.thr[c];
-    TrigState s = a.st[c];
-    int32_t win[kFirTaps];
-    win[0] = 0;
-#pragma unroll
-    for (int i = 1; i < kFirTaps; ++i) win[i] = a.rhist[(i - 1) * C + c];  // raw_{i-26}
-    int32_t n = 0;
-    uint64_t* slot = a.slots + (int64_t)c * a.capc;
-
-    for (int64_t g = 0; g < a.J; g += kFirTaps) {
-        const int64_t left = a.J - g;
-#pragma unroll
-        for (int u = 0; u < kFirTaps; ++u) {
-            if (u >= left) continue;  // tail group only; keeps the loop fully unrolled
-            const int64_t j = g + u;
-            win[u] = a.raw[j * C + c];
-            int32_t acc = 0;
-#pragma unroll
-            for (int i = 0; i < kFirTaps; ++i) acc += tap[i] * win[(u - i + kFirTaps) % kFirTaps];
-            const int32_t f = clamp16(acc >> 11);
-            if (!s.binit) {
-                s.B = (a.mode == MKID_BASE_NONE) ? 0 : f;
-                s.low = (int64_t)f << 16;
-                s.band = 0;
-                s.binit = 1;
-            }
-            const int32_t base_prev = (a.mode == MKID_BASE_SVF) ? (int32_t)(s.low >> 16) : s.B;
-            const int32_t e = f - base_prev;
-            const bool gate = (a.base_thr <= 0) || (e < a.base_thr && e > -a.base_thr);
-            if (a.mode == MKID_BASE_EMA && gate) {
-                s.B += (a.alpha * e) >> 9;
-            } else if (a.mode == MKID_BASE_SVF && gate) {
-                const int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)a.kq * s.band) >> 16);
-                s.band += ((int64_t)a.kf * high) >> 16;
-                s.low += ((int64_t)a.kf * s.band) >> 16;
-            }
-            if (s.st == ST_ARMED) {
-                if (e < thr) s.st = ST_PULSE;
-            } else if (s.st == ST_PULSE) {
-                if (f > s.f1) {
-                    const int64_t pk = peakfit_i(s.f2, s.f1, f);
-                    if (n < a.capc) slot[n] = pack_wide(c, pk, base_prev, a.j0 + j - 1);
-                    ++n;
-                    s.st = ST_DEAD;
-                    s.cnt = a.dead;
-                }
-            } else if (s.st == ST_DEAD) {
-                s.cnt -= 1;
-                if (s.cnt <= 0) s.st = ST_REARM;
-            } else {
-                if (e >= thr) s.st = ST_ARMED;
-            }
-            s.f2 = s.f1;
-            s.f1 = f;
+    const TrigCfg k{a.thr[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
+    TrigState T = a.s_end[c];  // segment 0 is exact
+    uint64_t* scratch = a.scratch + (int64_t)c * a.capseg;
+    int32_t reruns = 0;
+    for (int s = 1; s < a.nseg; ++s) {
+        const TrigState S0 = a.s_spec[(int64_t)s * C + c];
+        if (state_eq(T, S0, a.mode)) {
+            T = a.s_end[(int64_t)s * C + c];
+            continue;
         }
+        ++reruns;
+        const int64_t seg0 = (int64_t)s * a.L;
+        const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
+        TrigState tru = T, spc = S0;
+        int32_t nt = 0, ndrop = 0;
+        bool merged = false;
+        Win win;
+        load_window(win, a, c, seg0);
+        for (int64_t g = seg0; g < seg1 && !merged; g += kFirTaps) {
+            const int64_t left = seg1 - g;
+#pragma unroll
+            for (int u = 0; u < kFirTaps; ++u) {
+                if (u >= left || merged) continue;
+                const int64_t j = g + u;
+                win.w[u] = a.raw[j * C + c];
+                int32_t acc = 0;
+#pragma unroll
+                for (int i = 0; i < kFirTaps; ++i) acc += tap[i] * win.w[(u - i + kFirTaps) % kFirTaps];
+                const int32_t f = mf_out(acc);
+                uint64_t pkt;
+                if (trig_step(tru, f, k, c, a.j0 + j, &pkt)) {
+                    if (nt < a.capseg) scratch[nt] = pkt;
+                    ++nt;
+                }
+                uint64_t dummy;
+                if (trig_step(spc, f, k, c, a.j0 + j, &dummy)) ++ndrop;
+                merged = state_eq(tru, spc, a.mode);
+            }
+        }
+        const int64_t sc = (int64_t)c * a.nseg + s;
+        uint64_t* slot = a.slots + sc * a.capseg;
+        const int32_t cnt = a.counts[sc] < a.capseg ? a.counts[sc] : a.capseg;
+        int32_t total = nt;
+        if (merged) {
+            const int32_t keep = cnt - ndrop;  // speculative packets after the merge point
+            if (nt < ndrop) {
+                for (int32_t i = 0; i < keep; ++i) slot[nt + i] = slot[ndrop + i];
+            } else if (nt > ndrop) {
+                for (int32_t i = keep - 1; i >= 0; --i)
+                    if (nt + i < a.capseg) slot[nt + i] = slot[ndrop + i];
+            }
+            total = nt + (a.counts[sc] - ndrop);
+            T = a.s_end[(int64_t)s * C + c];
+        } else {
+            T = tru;
+        }
+        for (int32_t i = 0; i < nt && i < a.capseg; ++i) slot[i] = scratch[i];
+        a.counts[sc] = total;
     }
-    a.st[c] = s;
-    a.counts[c] = n;
+    a.st_out[c] = T;
+    if (a.reruns) a.reruns[c] = reruns;
 }
 
-hipError_t launch_trigger(const TrigArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_trigger, dim3((a.C + kTrigThreads - 1) / kTrigThreads), dim3(kTrigThreads),
-                       0, s, a);
+hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s) {
+    const unsigned cb = (a.C + kTrigThreads - 1) / kTrigThreads;
+    hipLaunchKernelGGL(k_trig_spec, dim3(cb, a.nseg), dim3(kTrigThreads), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_trig_fix, dim3(cb), dim3(kTrigThreads), 0, s, a);
     return hipGetLastError();
 }
 
-// ---- compaction: exclusive scan of per-channel counts (one block), then per-channel copy ----
+// ---- compaction: exclusive scan of (channel, segment) counts (one block), then copy ----------
 constexpr int kScanThreads = 1024;
 
 // d_counts[0] accumulates packets produced, d_counts[1] packets stored in `out` (<= cap), over
 // the sub-chunks of one process call (zeroed by the caller at the start of the call).
-__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* counts, int32_t C,
-                                                              int32_t capc, int64_t cap,
+__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* counts, int64_t n_ent,
+                                                              int32_t capseg, int64_t cap,
                                                               int64_t* offs, int64_t* d_counts) {
     __shared__ int64_t part[kScanThreads];
     __shared__ unsigned long long tot;
     const int64_t prev = d_counts[1];
-    const int per = (C + kScanThreads - 1) / kScanThreads;
-    const int b = threadIdx.x * per;
+    const int64_t per = (n_ent + kScanThreads - 1) / kScanThreads;
+    const int64_t b = threadIdx.x * per;
     int64_t sum = 0, sumw = 0;
-    for (int i = 0; i < per; ++i)
-        if (b + i < C) { const int v = counts[b + i]; sum += v; sumw += v < capc ? v : capc; }
+    for (int64_t i = 0; i < per; ++i)
+        if (b + i < n_ent) { const int v = counts[b + i]; sum += v; sumw += v < capseg ? v : capseg; }
     part[threadIdx.x] = sumw;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
@@ -129,8 +185,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* cou
         __syncthreads();
     }
     int64_t run = prev + part[threadIdx.x] - sumw;
-    for (int i = 0; i < per; ++i)
-        if (b + i < C) { offs[b + i] = run; const int v = counts[b + i]; run += v < capc ? v : capc; }
+    for (int64_t i = 0; i < per; ++i)
+        if (b + i < n_ent) { offs[b + i] = run; const int v = counts[b + i]; run += v < capseg ? v : capseg; }
     atomicAdd(&tot, (unsigned long long)sum);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -141,24 +197,26 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* cou
 }
 
 __global__ __launch_bounds__(256) void k_gather_events(const uint64_t* slots, const int32_t* counts,
-                                                       int32_t capc, const int64_t* offs,
-                                                       uint64_t* out, int64_t cap) {
-    const int c = blockIdx.x;
-    const int n = counts[c] < capc ? counts[c] : capc;
-    const int64_t o = offs[c];
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
-        if (o + i < cap) out[o + i] = slots[(int64_t)c * capc + i];
+                                                       int64_t n_ent, int32_t capseg,
+                                                       const int64_t* offs, uint64_t* out,
+                                                       int64_t cap) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_ent) return;
+    const int n = counts[e] < capseg ? counts[e] : capseg;
+    const int64_t o = offs[e];
+    for (int i = 0; i < n; ++i)
+        if (o + i < cap) out[o + i] = slots[e * capseg + i];
 }
 
-hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int32_t C, int32_t capc,
-                          uint64_t* out, int64_t cap, int64_t* d_counts, int64_t* scan_ws,
-                          hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, s, counts, C, capc, cap,
-                       scan_ws, d_counts);
+hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
+                          int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
+                          int64_t* scan_ws, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, s, counts, n_ent, capseg,
+                       cap, scan_ws, d_counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gather_events, dim3(C), dim3(256), 0, s, slots, counts, capc, scan_ws,
-                       out, cap);
+    hipLaunchKernelGGL(k_gather_events, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s,
+                       slots, counts, n_ent, capseg, scan_ws, out, cap);
     return hipGetLastError();
 }
 

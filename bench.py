@@ -160,18 +160,12 @@ def main():
 
     phase = None if args.no_phase else torch.empty(J * C, dtype=torch.float32, device=dev)
 
+    from mkids_sdr_amd.feedlines import gather_packets
+
     def step():
         ch.process_device(x, S, phase, d_events, cap, d_counts)
         if world > 1:   # photon-list gather to rank 0 (the path's one exchange step)
-            cnt = d_counts[1:2].clone()
-            allc = [torch.zeros_like(cnt) for _ in range(world)]
-            dist.all_gather(allc, cnt)
-            mx = int(torch.stack(allc).max().item())
-            buf = torch.zeros(max(mx, 1), dtype=torch.int64, device=dev)
-            n = int(cnt.item())
-            buf[:n] = d_events[:n]
-            bufs = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-            dist.gather(buf, bufs, dst=0)
+            gather_packets(d_events, int(d_counts[1].item()), dst=0)
 
     for _ in range(args.warmup):
         step()

@@ -84,15 +84,17 @@ EXPORTS = sorted(list(_SIGS) + ['mkid_last_error', 'mkid_global_error', 'mkid_ke
 _lib = None
 
 
-def load():
-    """Load the in-tree HIP library; raise if it was not built."""
+def load(path=None):
+    """Load the in-tree HIP library; raise if it was not built. `path` loads a build variant
+    (tools/kbench.py) as a separate library instance."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    lp = path or LIB_PATH
+    if not os.path.exists(lp):
         raise ImportError('libmkidgpu.so not built at %s: run __graft_entry__.build() '
-                          '(make -C mkids_sdr_amd/csrc); there is no CPU fallback' % LIB_PATH)
-    L = ctypes.CDLL(LIB_PATH)
+                          '(make -C mkids_sdr_amd/csrc); there is no CPU fallback' % lp)
+    L = ctypes.CDLL(lp)
     for name, args in _SIGS.items():
         f = getattr(L, name)
         f.argtypes = args
@@ -104,7 +106,8 @@ def load():
     L.mkid_global_error.restype = ctypes.c_char_p
     L.mkid_kernel_name.argtypes = [I32]
     L.mkid_kernel_name.restype = ctypes.c_char_p
-    _lib = L
+    if path is None:
+        _lib = L
     return L
 
 

@@ -26,8 +26,8 @@ def _ptr(a):
 
 class Channelizer:
     def __init__(self, n_channels, device=0, max_chunk=1 << 22, dead_time=32, sample_rate=512e6,
-                 max_events_per_ch=0):
-        self._L = _lib.load()
+                 max_events_per_ch=0, lib_path=None):
+        self._L = _lib.load(lib_path)
         cfg = _lib.Cfg()
         _lib.check(self._L.mkid_default_cfg(ctypes.byref(cfg), int(n_channels)))
         cfg.max_chunk = int(max_chunk)
@@ -56,7 +56,10 @@ class Channelizer:
             pass
 
     def _chk(self, rc):
-        return _lib.check(rc, self._h)
+        if rc != _lib.MKID_OK:
+            msg = (self._L.mkid_last_error(self._h) or b'').decode(errors='replace')
+            raise _lib.MkidError(rc, msg)
+        return rc
 
     # ---- configuration (one register group each) ---------------------------------------------
     def set_stream(self, stream_ptr):

@@ -113,13 +113,13 @@ def center_register(ic, qc):
 
 def decode_center_register(w):
     """Inverse of center_register for |I/8|,|Q/8| < 2^15 (handles the unmasked negative Q)."""
-    w = int(w)
+    w = int(w) & 0xFFFFFFFF
+    if w & 0x80000000:
+        w -= 1 << 32               # the register is a signed 32-bit write_int value
     q16 = w & 0xFFFF
     if q16 & 0x8000:
         q16 -= 0x10000
-    i16 = (w - q16) >> 16
-    if i16 & 0x8000:
-        i16 -= 0x10000
+    i16 = (w - q16) >> 16          # arithmetic: already signed
     return 8.0 * i16, 8.0 * q16
 
 

@@ -55,7 +55,10 @@ __device__ __forceinline__ uint4 load_new(const ChanArgs& a, int64_t first_hop, 
 }
 
 template <int N>
-__global__ __launch_bounds__(Geo<N>::BT) void k_channelize(ChanArgs a) {
+#ifndef MKID_CHAN_MINWAVES
+#define MKID_CHAN_MINWAVES 1
+#endif
+__global__ __launch_bounds__(Geo<N>::BT, MKID_CHAN_MINWAVES) void k_channelize(ChanArgs a) {
     using G = Geo<N>;
     using PL = Plan8<N>;
     constexpr int PTS = G::PTS, NT = G::NT, M = G::M, C = G::C, T = G::T, RS = G::RS;

@@ -5,73 +5,150 @@
 //                channel's carried state (exact). Segment s>0 starts W samples early from a guessed
 //                state (re-arm pending, baseline = first filtered sample), runs the warm-up
 //                silently, records its state S_spec at the segment start, then emits packets.
-//   k_trig_fix   thread = channel. Walks the segments in order with the true state T. If
-//                T == S_spec (canonical compare) the segment's packets are exact. Otherwise it
-//                re-runs the true and the speculative trajectories side by side from the segment
-//                start until they coincide (the recurrence is deterministic in (state, input)), and
-//                splices: true packets before the merge + speculative packets after it.
-//   compaction   exclusive scan over (channel, segment) counts -> channel-major, time-ascending.
+//   k_trig_fix   one wave per channel. Segment s is exact iff the true state at its start equals
+//                S_spec[s]; by induction from the exact segment 0 that is S_end[s-1] == S_spec[s],
+//                checked for all segments at once (64 per ballot). Only the failures walk
+//                serially: the true and the speculative trajectories are re-run side by side from
+//                the segment start until they coincide (the recurrence is deterministic in
+//                (state, input)) and the packet lists are spliced: true packets before the merge,
+//                speculative ones after it. A re-run that never merges hands its end state to an
+//                explicit check of the next segment.
 //
 // The result is bit-identical to the sequential oracle/trigger.c for every input; the speculation
 // only decides how much sequential work the fix-up does (EMA merges within ~10^2 samples on noisy
-// phase). SVF mode (slow 2-pole baseline with a wide dead band) uses one segment = serial.
+// phase). SVF mode (slow 2-pole baseline with a wide dead band) runs as one exact segment.
+// The 26-tap matched filter uses 24-bit multiply-adds (taps are 12-bit, samples 16-bit).
 #include "trig_common.h"
 
 namespace mkid {
 
-constexpr int kTrigThreads = 64;
+constexpr int kSpecThreads = 256;
+
+__device__ __attribute__((noinline)) uint64_t make_packet(int32_t c, EvInfo ev, int32_t f, int64_t jg) {
+    return pack_wide(c, peakfit_i(ev.y1, ev.y2, f), ev.base, jg - 1);
+}
 
 struct Win {
     int32_t w[kFirTaps];
 };
 
-// Prologue: load raw_{j-25..j-1} into ring slots (j' - j + 26) % 26 for a ring aligned at j.
+// Load raw_{j-25..j-1} into ring slots (j' - j + 26) % 26 of a ring aligned at j.
 __device__ __forceinline__ void load_window(Win& win, const TrigSpecArgs& a, int c, int64_t j) {
     win.w[0] = 0;
 #pragma unroll
     for (int i = 1; i < kFirTaps; ++i) {
         const int64_t jj = j - kFirTaps + i;  // slot i holds raw_{j-26+i}
-        win.w[i] = jj >= 0 ? a.raw[jj * a.C + c] : (jj >= -kRawHist ? a.rhist[(jj + kRawHist) * a.C + c] : 0);
+        win.w[i] = jj >= 0 ? a.raw[jj * a.C + c]
+                           : (jj >= -kRawHist ? a.rhist[(jj + kRawHist) * a.C + c] : 0);
     }
 }
 
-__global__ __launch_bounds__(kTrigThreads) void k_trig_spec(TrigSpecArgs a) {
-    const int c = blockIdx.x * kTrigThreads + threadIdx.x;
-    const int s = blockIdx.y;
-    if (c >= a.C) return;
-    const int C = a.C;
-    int32_t tap[kFirTaps];
+// filtered sample for ring position u (raw_j already stored in slot u)
+__device__ __forceinline__ int32_t mf_at(const Win& win, const int32_t (&tap)[kFirTaps], int u) {
+    int32_t acc = 0;
 #pragma unroll
-    for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
-    const TrigCfg k{a.thr[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
+    for (int i = 0; i < kFirTaps; ++i) acc = __mul24(tap[i], win.w[(u - i + kFirTaps) % kFirTaps]) + acc;
+    return mf_out(acc);
+}
+
+// Matched filter on packed pairs: q_j = (raw_j, raw_{j-1}) as two int16 in one dword, and
+// tap pairs (a_2m, a_2m+1); f_j = sum_m dot2(tappair_m, q_{j-2m}) -> 13 v_dot2c_i32_i16 per sample.
+typedef short short2_t __attribute__((ext_vector_type(2)));
+struct QWin {
+    uint32_t q[kFirTaps];  // slot (i - base) % 26 holds q_i
+    int32_t last;          // raw_{i-1} for the next pack
+};
+
+__device__ __forceinline__ uint32_t pack2(int32_t lo, int32_t hi) {
+    return ((uint32_t)lo & 0xffffu) | ((uint32_t)hi << 16);
+}
+
+__device__ __forceinline__ short2_t as_s2(uint32_t v) { return __builtin_bit_cast(short2_t, v); }
+
+// ring aligned at j: slots 2..25 hold q_{j-24..j-1} (slot (i - j + 26) % 26); last = raw_{j-1}
+__device__ __forceinline__ void load_qwin(QWin& w, const TrigSpecArgs& a, int c, int64_t j) {
+    int32_t prev = 0;
+#pragma unroll
+    for (int i = 0; i < kFirTaps; ++i) {
+        const int64_t jj = j - kFirTaps + i;  // raw_{j-26+i}
+        const int32_t r = jj >= 0 ? a.raw[jj * a.C + c]
+                                  : (jj >= -kRawHist ? a.rhist[(jj + kRawHist) * a.C + c] : 0);
+        w.q[i] = pack2(r, prev);
+        prev = r;
+    }
+    w.last = prev;
+}
+
+__device__ __forceinline__ int32_t mf_q(QWin& w, const uint32_t (&tp)[kFirTaps / 2], int u, int32_t r) {
+    w.q[u] = pack2(r, w.last);
+    w.last = r;
+    int32_t acc = 0;
+#pragma unroll
+    for (int m = 0; m < kFirTaps / 2; ++m)
+        acc = __builtin_amdgcn_sdot2(as_s2(tp[m]), as_s2(w.q[(u - 2 * m + 2 * kFirTaps) % kFirTaps]), acc, false);
+    return mf_out(acc);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kSpecThreads) void k_trig_spec(TrigSpecArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * kSpecThreads + threadIdx.x;
+    if (g >= (int64_t)a.C * a.nseg) return;
+    const int C = a.C;
+    const int c = (int)(g % C);  // lanes of a wave = consecutive channels (coalesced raw loads)
+    const int s = (int)(g / C);
+    uint32_t tp[kFirTaps / 2];
+#pragma unroll
+    for (int m = 0; m < kFirTaps / 2; ++m) tp[m] = pack2(a.fir[c * kFirTaps + 2 * m], a.fir[c * kFirTaps + 2 * m + 1]);
+    const TrigCfg k{a.thr[c], MODE, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
     const int64_t seg0 = (int64_t)s * a.L;
     const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
     const int64_t jw = s == 0 ? 0 : seg0 - a.W;
-    TrigState st;
-    if (s == 0) {
-        st = a.st_in[c];
-    } else {
-        st = TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
-    }
-    Win win;
-    load_window(win, a, c, jw);
+    TrigState st = s == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
+    QWin win;
+    load_qwin(win, a, c, jw);
     const int64_t sc = (int64_t)c * a.nseg + s;
     uint64_t* slot = a.slots + sc * a.capseg;
     int32_t n = 0;
-    for (int64_t g = jw; g < seg1; g += kFirTaps) {
-        const int64_t left = seg1 - g;
+    const int16_t* rp = a.raw + jw * C + c;  // running pointer: no 64-bit index multiplies
+    // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0
+    for (int32_t gi = 0; gi < (int32_t)(seg0 - jw); gi += kFirTaps) {
+        int32_t r[kFirTaps];
+#pragma unroll
+        for (int u = 0; u < kFirTaps; ++u) r[u] = rp[(int64_t)u * C];  // all loads in flight
+        rp += (int64_t)kFirTaps * C;
 #pragma unroll
         for (int u = 0; u < kFirTaps; ++u) {
-            if (u >= left) continue;
-            const int64_t j = g + u;
-            win.w[u] = a.raw[j * C + c];
-            int32_t acc = 0;
+            EvInfo ev;
+            (void)trig_update(st, mf_q(win, tp, u, r[u]), k, ev);
+        }
+    }
+    if (s > 0) a.s_spec[(int64_t)s * C + c] = st;
+    const int32_t len = (int32_t)(seg1 - seg0);
+    const int32_t full = len - len % kFirTaps;
+    int32_t gi = 0;
+    for (; gi < full; gi += kFirTaps) {
+        int32_t r[kFirTaps];
 #pragma unroll
-            for (int i = 0; i < kFirTaps; ++i) acc += tap[i] * win.w[(u - i + kFirTaps) % kFirTaps];
-            if (s > 0 && j == seg0) a.s_spec[(int64_t)s * C + c] = st;
-            uint64_t pkt;
-            if (trig_step(st, mf_out(acc), k, c, a.j0 + j, &pkt) && j >= seg0) {
-                if (n < a.capseg) slot[n] = pkt;
+        for (int u = 0; u < kFirTaps; ++u) r[u] = rp[(int64_t)u * C];
+        rp += (int64_t)kFirTaps * C;
+#pragma unroll
+        for (int u = 0; u < kFirTaps; ++u) {
+            const int32_t f = mf_q(win, tp, u, r[u]);
+            EvInfo ev;
+            if (trig_update(st, f, k, ev)) {
+                if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);
+                ++n;
+            }
+        }
+    }
+    const int32_t left = len - gi;  // tail < 26 samples, predicated
+#pragma unroll
+    for (int u = 0; u < kFirTaps; ++u) {
+        if (u < left) {
+            const int32_t f = mf_q(win, tp, u, rp[(int64_t)u * C]);
+            EvInfo ev;
+            if (trig_update(st, f, k, ev)) {
+                if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);
                 ++n;
             }
         }
@@ -80,166 +157,119 @@ __global__ __launch_bounds__(kTrigThreads) void k_trig_spec(TrigSpecArgs a) {
     a.counts[sc] = n;
 }
 
-__global__ __launch_bounds__(kTrigThreads) void k_trig_fix(TrigSpecArgs a) {
-    const int c = blockIdx.x * kTrigThreads + threadIdx.x;
-    if (c >= a.C) return;
+// Re-run segment s of channel c from the true state T and the speculative state S0 side by side.
+// Returns true if they merged; T becomes the true state at the segment end when they did not.
+__device__ bool rerun_segment(const TrigSpecArgs& a, int c, int s, const int32_t (&tap)[kFirTaps],
+                              const TrigCfg& k, TrigState& T, const TrigState& S0) {
+    const int64_t seg0 = (int64_t)s * a.L;
+    const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
+    uint64_t* scratch = a.scratch + (int64_t)c * a.capseg;
+    TrigState tru = T, spc = S0;
+    int32_t nt = 0, ndrop = 0;
+    bool merged = false;
+    Win win;
+    load_window(win, a, c, seg0);
+    const int16_t* rp = a.raw + seg0 * a.C + c;
+    for (int64_t g = seg0; g < seg1 && !merged; g += kFirTaps) {
+        const int64_t left = seg1 - g;
+#pragma unroll
+        for (int u = 0; u < kFirTaps; ++u) {
+            if (u >= left || merged) continue;
+            const int64_t j = g + u;
+            win.w[u] = *rp;
+            rp += a.C;
+            const int32_t f = mf_at(win, tap, u);
+            uint64_t pkt;
+            if (trig_step(tru, f, k, c, a.j0 + j, &pkt)) {
+                if (nt < a.capseg) scratch[nt] = pkt;
+                ++nt;
+            }
+            uint64_t dummy;
+            if (trig_step(spc, f, k, c, a.j0 + j, &dummy)) ++ndrop;
+            merged = state_eq(tru, spc, a.mode);
+        }
+    }
+    const int64_t sc = (int64_t)c * a.nseg + s;
+    uint64_t* slot = a.slots + sc * a.capseg;
+    const int32_t cnt = a.counts[sc] < a.capseg ? a.counts[sc] : a.capseg;
+    int32_t total = nt;
+    if (merged) {
+        const int32_t keep = cnt - ndrop;  // speculative packets after the merge point
+        if (nt < ndrop) {
+            for (int32_t i = 0; i < keep; ++i) slot[nt + i] = slot[ndrop + i];
+        } else if (nt > ndrop) {
+            for (int32_t i = keep - 1; i >= 0; --i)
+                if (nt + i < a.capseg) slot[nt + i] = slot[ndrop + i];
+        }
+        total = nt + (a.counts[sc] - ndrop);
+    } else {
+        T = tru;
+    }
+    for (int32_t i = 0; i < nt && i < a.capseg; ++i) slot[i] = scratch[i];
+    a.counts[sc] = total;
+    return merged;
+}
+
+__global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
+    extern __shared__ uint64_t okbits[];  // bit s%64 of word s/64: segment s needs no re-run
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
     const int C = a.C;
+    const int nwords = (a.nseg + 63) / 64;
+    for (int wd = 0; wd < nwords; ++wd) {
+        const int s = wd * 64 + lane;
+        bool ok = true;
+        if (s >= 1 && s < a.nseg)
+            ok = state_eq(a.s_end[(int64_t)(s - 1) * C + c], a.s_spec[(int64_t)s * C + c], a.mode);
+        const uint64_t b = __ballot(ok);
+        if (lane == 0) okbits[wd] = b;
+    }
+    __syncthreads();
+    if (lane != 0) return;
     int32_t tap[kFirTaps];
 #pragma unroll
     for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
     const TrigCfg k{a.thr[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
-    TrigState T = a.s_end[c];  // segment 0 is exact
-    uint64_t* scratch = a.scratch + (int64_t)c * a.capseg;
+    TrigState T{};
+    bool override_ = false;  // T holds the true start state of segment s (from an unmerged re-run)
     int32_t reruns = 0;
-    for (int s = 1; s < a.nseg; ++s) {
-        const TrigState S0 = a.s_spec[(int64_t)s * C + c];
-        if (state_eq(T, S0, a.mode)) {
-            T = a.s_end[(int64_t)s * C + c];
+    int s = 1;
+    while (s < a.nseg) {
+        if (!override_) {
+            // next segment whose precomputed check failed
+            int wd = s >> 6;
+            uint64_t fail = ~okbits[wd] & (~0ull << (s & 63));
+            while (!fail && ++wd < nwords) fail = ~okbits[wd];
+            if (!fail) break;
+            s = wd * 64 + __builtin_ctzll(fail);
+            if (s >= a.nseg) break;
+            T = a.s_end[(int64_t)(s - 1) * C + c];
+        } else if (state_eq(T, a.s_spec[(int64_t)s * C + c], a.mode)) {
+            override_ = false;
+            ++s;
             continue;
         }
         ++reruns;
-        const int64_t seg0 = (int64_t)s * a.L;
-        const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
-        TrigState tru = T, spc = S0;
-        int32_t nt = 0, ndrop = 0;
-        bool merged = false;
-        Win win;
-        load_window(win, a, c, seg0);
-        for (int64_t g = seg0; g < seg1 && !merged; g += kFirTaps) {
-            const int64_t left = seg1 - g;
-#pragma unroll
-            for (int u = 0; u < kFirTaps; ++u) {
-                if (u >= left || merged) continue;
-                const int64_t j = g + u;
-                win.w[u] = a.raw[j * C + c];
-                int32_t acc = 0;
-#pragma unroll
-                for (int i = 0; i < kFirTaps; ++i) acc += tap[i] * win.w[(u - i + kFirTaps) % kFirTaps];
-                const int32_t f = mf_out(acc);
-                uint64_t pkt;
-                if (trig_step(tru, f, k, c, a.j0 + j, &pkt)) {
-                    if (nt < a.capseg) scratch[nt] = pkt;
-                    ++nt;
-                }
-                uint64_t dummy;
-                if (trig_step(spc, f, k, c, a.j0 + j, &dummy)) ++ndrop;
-                merged = state_eq(tru, spc, a.mode);
-            }
-        }
-        const int64_t sc = (int64_t)c * a.nseg + s;
-        uint64_t* slot = a.slots + sc * a.capseg;
-        const int32_t cnt = a.counts[sc] < a.capseg ? a.counts[sc] : a.capseg;
-        int32_t total = nt;
-        if (merged) {
-            const int32_t keep = cnt - ndrop;  // speculative packets after the merge point
-            if (nt < ndrop) {
-                for (int32_t i = 0; i < keep; ++i) slot[nt + i] = slot[ndrop + i];
-            } else if (nt > ndrop) {
-                for (int32_t i = keep - 1; i >= 0; --i)
-                    if (nt + i < a.capseg) slot[nt + i] = slot[ndrop + i];
-            }
-            total = nt + (a.counts[sc] - ndrop);
-            T = a.s_end[(int64_t)s * C + c];
-        } else {
-            T = tru;
-        }
-        for (int32_t i = 0; i < nt && i < a.capseg; ++i) slot[i] = scratch[i];
-        a.counts[sc] = total;
+        override_ = !rerun_segment(a, c, s, tap, k, T, a.s_spec[(int64_t)s * C + c]);
+        ++s;
     }
-    a.st_out[c] = T;
+    a.st_out[c] = override_ ? T : a.s_end[(int64_t)(a.nseg - 1) * C + c];
     if (a.reruns) a.reruns[c] = reruns;
 }
 
 hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s) {
-    const unsigned cb = (a.C + kTrigThreads - 1) / kTrigThreads;
-    hipLaunchKernelGGL(k_trig_spec, dim3(cb, a.nseg), dim3(kTrigThreads), 0, s, a);
+    const int64_t threads = (int64_t)a.C * a.nseg;
+    const dim3 grid((unsigned)((threads + kSpecThreads - 1) / kSpecThreads));
+    if (a.mode == MKID_BASE_EMA)
+        hipLaunchKernelGGL(k_trig_spec<MKID_BASE_EMA>, grid, dim3(kSpecThreads), 0, s, a);
+    else if (a.mode == MKID_BASE_SVF)
+        hipLaunchKernelGGL(k_trig_spec<MKID_BASE_SVF>, grid, dim3(kSpecThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_trig_spec<MKID_BASE_NONE>, grid, dim3(kSpecThreads), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_trig_fix, dim3(cb), dim3(kTrigThreads), 0, s, a);
-    return hipGetLastError();
-}
-
-// ---- compaction: exclusive scan of (channel, segment) counts (one block), then copy ----------
-constexpr int kScanThreads = 1024;
-
-// d_counts[0] accumulates packets produced, d_counts[1] packets stored in `out` (<= cap), over
-// the sub-chunks of one process call (zeroed by the caller at the start of the call).
-__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* counts, int64_t n_ent,
-                                                              int32_t capseg, int64_t cap,
-                                                              int64_t* offs, int64_t* d_counts) {
-    __shared__ int64_t part[kScanThreads];
-    __shared__ unsigned long long tot;
-    const int64_t prev = d_counts[1];
-    const int64_t per = (n_ent + kScanThreads - 1) / kScanThreads;
-    const int64_t b = threadIdx.x * per;
-    int64_t sum = 0, sumw = 0;
-    for (int64_t i = 0; i < per; ++i)
-        if (b + i < n_ent) { const int v = counts[b + i]; sum += v; sumw += v < capseg ? v : capseg; }
-    part[threadIdx.x] = sumw;
-    if (threadIdx.x == 0) tot = 0;
-    __syncthreads();
-    for (int off = 1; off < kScanThreads; off <<= 1) {  // Hillis-Steele inclusive scan
-        const int64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    int64_t run = prev + part[threadIdx.x] - sumw;
-    for (int64_t i = 0; i < per; ++i)
-        if (b + i < n_ent) { offs[b + i] = run; const int v = counts[b + i]; run += v < capseg ? v : capseg; }
-    atomicAdd(&tot, (unsigned long long)sum);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        d_counts[0] += (int64_t)tot;
-        const int64_t w = prev + part[kScanThreads - 1];
-        d_counts[1] = w < cap ? w : cap;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_gather_events(const uint64_t* slots, const int32_t* counts,
-                                                       int64_t n_ent, int32_t capseg,
-                                                       const int64_t* offs, uint64_t* out,
-                                                       int64_t cap) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n_ent) return;
-    const int n = counts[e] < capseg ? counts[e] : capseg;
-    const int64_t o = offs[e];
-    for (int i = 0; i < n; ++i)
-        if (o + i < cap) out[o + i] = slots[e * capseg + i];
-}
-
-hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
-                          int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
-                          int64_t* scan_ws, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, s, counts, n_ent, capseg,
-                       cap, scan_ws, d_counts);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gather_events, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s,
-                       slots, counts, n_ent, capseg, scan_ws, out, cap);
-    return hipGetLastError();
-}
-
-// ---- history roll: dst[i] = concat(old[0:hist_rows], fresh[0:fresh_rows])[fresh_rows + i] ----
-__global__ void k_hist_roll(uint8_t* dst, const uint8_t* old_hist, const uint8_t* fresh,
-                            int64_t hist_rows, int64_t fresh_rows, int64_t row_bytes) {
-    const int64_t total = hist_rows * row_bytes;
-    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total;
-         b += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t row = b / row_bytes, col = b % row_bytes;
-        const int64_t src = fresh_rows + row;  // index into concat
-        dst[b] = src < hist_rows ? old_hist[src * row_bytes + col]
-                                 : fresh[(src - hist_rows) * row_bytes + col];
-    }
-}
-
-hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
-                            int64_t fresh_rows, int64_t row_bytes, hipStream_t s) {
-    const int64_t total = hist_rows * row_bytes;
-    const int blocks = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
-    hipLaunchKernelGGL(k_hist_roll, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, (uint8_t*)dst,
-                       (const uint8_t*)old_hist, (const uint8_t*)fresh, hist_rows, fresh_rows,
-                       row_bytes);
+    const size_t lds = (size_t)((a.nseg + 63) / 64) * 8;
+    hipLaunchKernelGGL(k_trig_fix, dim3(a.C), dim3(64), lds, s, a);
     return hipGetLastError();
 }
 

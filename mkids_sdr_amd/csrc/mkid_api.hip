@@ -32,7 +32,8 @@ struct KTime {
 // speculating from kSegW samples of warm-up. The EMA baseline (alpha 41/512) forgets its start
 // in ~10^2 samples on noisy phase; SVF runs as a single exact segment.
 constexpr int64_t kSegL = 2048;
-constexpr int64_t kSegW = 512;
+constexpr int64_t kSegW = 520;  // multiple of the 26-sample matched-filter ring
+static_assert(kSegW % kFirTaps == 0 && kSegL >= kSegW + kRawHist, "segment geometry");
 int64_t seg_capacity(int dead) { return kSegL / (dead + 3) + 2; }
 
 }  // namespace

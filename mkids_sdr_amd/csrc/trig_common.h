@@ -31,10 +31,19 @@ __device__ __forceinline__ uint64_t pack_wide(int32_t ch, int64_t peak, int32_t 
 // Matched-filter output from the 26-sample window: tap i multiplies raw_{j-i}.
 __device__ __forceinline__ int32_t mf_out(int32_t acc) { return tclamp16(acc >> 11); }
 
-// Advance state s by one filtered sample f taken at global phase index jg. Returns true and fills
-// *pkt when a packet is emitted (its timestamp is jg - 1: the peak is the previous sample).
-__device__ __forceinline__ bool trig_step(TrigState& s, int32_t f, const TrigCfg& k, int32_t c,
-                                          int64_t jg, uint64_t* pkt) {
+// What a packet needs besides the current sample: the two previous filtered samples and the
+// baseline the trigger compared against.
+struct EvInfo {
+    int32_t y1, y2, base;
+};
+
+// Packet assembly is out of line: it runs once per event (int64 parabolic fit with a division),
+// and keeping it out of the 26-fold unrolled sample loops keeps those loops small.
+__device__ __attribute__((noinline)) uint64_t make_packet(int32_t c, EvInfo ev, int32_t f, int64_t jg);
+
+// Advance state s by one filtered sample f. Returns true when a packet is due; ev then holds
+// its inputs (the packet is stamped jg - 1: the peak is the previous sample).
+__device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigCfg& k, EvInfo& ev) {
     if (!s.binit) {
         s.B = (k.mode == MKID_BASE_NONE) ? 0 : f;
         s.low = (int64_t)f << 16;
@@ -44,32 +53,37 @@ __device__ __forceinline__ bool trig_step(TrigState& s, int32_t f, const TrigCfg
     const int32_t base_prev = (k.mode == MKID_BASE_SVF) ? (int32_t)(s.low >> 16) : s.B;
     const int32_t e = f - base_prev;
     const bool gate = (k.base_thr <= 0) || (e < k.base_thr && e > -k.base_thr);
-    if (k.mode == MKID_BASE_EMA && gate) {
-        s.B += (k.alpha * e) >> 9;
+    if (k.mode == MKID_BASE_EMA) {
+        s.B += gate ? ((k.alpha * e) >> 9) : 0;
     } else if (k.mode == MKID_BASE_SVF && gate) {
         const int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)k.kq * s.band) >> 16);
         s.band += ((int64_t)k.kf * high) >> 16;
         s.low += ((int64_t)k.kf * s.band) >> 16;
     }
-    bool emit = false;
-    if (s.st == ST_ARMED) {
-        if (e < k.thr) s.st = ST_PULSE;
-    } else if (s.st == ST_PULSE) {
-        if (f > s.f1) {
-            *pkt = pack_wide(c, peakfit_i(s.f2, s.f1, f), base_prev, jg - 1);
-            emit = true;
-            s.st = ST_DEAD;
-            s.cnt = k.dead;
-        }
-    } else if (s.st == ST_DEAD) {
-        s.cnt -= 1;
-        if (s.cnt <= 0) s.st = ST_REARM;
-    } else {
-        if (e >= k.thr) s.st = ST_ARMED;
-    }
+    // state machine as selects: lanes are channels in different states, branches would diverge
+    const bool armed = s.st == ST_ARMED, pulse = s.st == ST_PULSE, dead = s.st == ST_DEAD;
+    const bool rearm = s.st == ST_REARM;
+    const bool emit = pulse && (f > s.f1);
+    const int32_t cnt1 = s.cnt - 1;
+    const bool to_pulse = armed && (e < k.thr);
+    const bool to_rearm = dead && (cnt1 <= 0);
+    const bool to_armed = rearm && (e >= k.thr);
+    ev = EvInfo{s.f2, s.f1, base_prev};
+    s.cnt = emit ? k.dead : (dead ? cnt1 : s.cnt);
+    s.st = to_pulse ? ST_PULSE : (emit ? ST_DEAD : (to_rearm ? ST_REARM : (to_armed ? ST_ARMED : s.st)));
     s.f2 = s.f1;
     s.f1 = f;
     return emit;
+}
+
+// Advance state s by one filtered sample f taken at global phase index jg. Returns true and fills
+// *pkt when a packet is emitted (its timestamp is jg - 1: the peak is the previous sample).
+__device__ __forceinline__ bool trig_step(TrigState& s, int32_t f, const TrigCfg& k, int32_t c,
+                                          int64_t jg, uint64_t* pkt) {
+    EvInfo ev;
+    if (!trig_update(s, f, k, ev)) return false;
+    *pkt = make_packet(c, ev, f, jg);
+    return true;
 }
 
 // Equality of the parts of the state that influence future outputs (dead-time counter only in

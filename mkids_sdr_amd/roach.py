@@ -1,0 +1,416 @@
+"""FpgaClient-compatible register shim + the ChannelizerControls setup surface, over the GPU.
+
+The reference drives its firmware with ``corr.katcp_wrapper.FpgaClient(ip, 7147)`` and five calls
+(ROACH_Setup.py:112-115, 545-547, 570, 603-605, 659, 887; ROACH_Pulses.py:95-97, 242-248,
+286-288, 796-800): ``progdev``, ``write_int``, ``write``, ``read``, ``read_int``. ``FpgaClient``
+below accepts exactly those calls and register names, decodes every configuration write into
+the device configuration of one MI355X channeliser context (include/mkidgpu.h), and serves the
+readback registers from the GPU's outputs on a DAC->ADC loop-back source (the conjugated DAC LUT,
+ROACH_Setup.py:485-487). ``RoachSetup`` / ``RoachPulses`` restate the reference's AppForm methods
+(same names and argument meaning, GUI widgets replaced by attributes) on top of it, so
+ChannelizerControls-style code runs unchanged against the GPU.
+
+Register map:
+  config   bins/load_bins, dram_memory, FIR_b{2n}b{2n+1}/FIR_load_coeff, capture_threshold/
+           capture_load_thresh, conv_phase_centers/conv_phase_load_centers,
+           capture_Baseline_alpha, capture_base_Kf, capture_base_Kq, capture_base_thresh
+  control  startDAC, DRAM_LUT_rd_valid, startAccumulator, avgIQ_ctrl, startSnap, snapPhase_ctrl,
+           ch_we, startBuffer
+  readback avgIQ_bram, snapPhase_bram, pulses_addr, pulses_bram0/1
+Errors are raised as RuntimeError (katcp semantics, pulse_triggering_v2.py:177-179).
+"""
+import re
+import struct
+
+import numpy as np
+
+from . import codecs, lut
+
+FIR_RE = re.compile(r'^FIR_b(\d+)b(\d+)$')
+PULSE_RING = 2 ** 14          # pulses_bram0/1 depth (ROACH_Pulses.py:799-800)
+
+
+class DeviceConfig:
+    """Decoded firmware configuration (pure host state; pushed to a Channelizer by sync())."""
+
+    def __init__(self, n_channels, dds_lag=lut.DDS_LAG):
+        C = n_channels
+        self.C = C
+        self.dds_lag = dds_lag
+        self.bins = np.arange(C, dtype=np.int64)
+        self.lut_i = np.full((C, lut.LUT_LEN // C), 32767, np.int64)
+        self.lut_q = np.zeros((C, lut.LUT_LEN // C), np.int64)
+        self.dac_i = np.zeros(lut.LUT_LEN, np.int64)
+        self.dac_q = np.zeros(lut.LUT_LEN, np.int64)
+        self.fir = np.zeros((C, 26), np.int64)
+        self.thr = np.full(C, -(1 << 30), np.int64)
+        self.ic = np.zeros(C, np.float32)
+        self.qc = np.zeros(C, np.float32)
+        self.baseline = dict(mode=1, alpha=41, kf=82, kq=93623, base_thr=8192)
+        self.dirty = set(['bins', 'dds', 'fir', 'thr', 'centers', 'baseline'])
+
+
+class FpgaClient:
+    """katcp FpgaClient look-alike over one GPU channeliser context."""
+
+    def __init__(self, host='mi355x', port=7147, n_channels=256, device=0, sample_rate=512e6,
+                 dds_lag=lut.DDS_LAG, gpu=True, noise_sigma=0.0, seed=0):
+        self.host, self.port = host, port
+        self.C = n_channels
+        self.N = 2 * n_channels
+        self.fs = sample_rate
+        self.device = device
+        self.regs = {}
+        self.cfg = DeviceConfig(n_channels, dds_lag)
+        self.gpu = gpu
+        self.noise_sigma = noise_sigma
+        self.rng = np.random.default_rng(seed)
+        self._chan = None
+        self._t = 0                      # loop-back source position (ADC samples)
+        self._ring = np.zeros(PULSE_RING, np.uint64)
+        self._addr = 0
+        self._buffering = False
+        self.boffile = None
+
+    # ---- katcp surface -----------------------------------------------------------------------
+    def progdev(self, boffile):
+        self.boffile = boffile
+        self.regs.clear()
+        self.cfg = DeviceConfig(self.C, self.cfg.dds_lag)
+        self._t = 0
+        if self._chan is not None:
+            self._chan.reset()
+        return 'ok'
+
+    def is_connected(self):
+        return True
+
+    def listdev(self):
+        return sorted(self.regs)
+
+    def write_int(self, name, value, blindwrite=False, offset=0):
+        value = int(value)
+        prev = self.regs.get(name, 0)
+        self.regs[name] = value
+        rising = (value & 1) and not (prev & 1)
+        if name == 'load_bins' and rising:
+            self.cfg.bins[value >> 1] = self.regs.get('bins', 0) % self.N
+            self.cfg.dirty.add('bins')
+        elif name == 'FIR_load_coeff' and rising:
+            ch = value >> 1
+            for n in range(13):
+                key = 'FIR_b%db%d' % (2 * n, 2 * n + 1)
+                if key in self.regs:
+                    self.cfg.fir[ch, 2 * n], self.cfg.fir[ch, 2 * n + 1] = \
+                        codecs.decode_fir_register(self.regs[key])
+            self.cfg.dirty.add('fir')
+        elif name == 'capture_load_thresh' and rising:
+            self.cfg.thr[value >> 1] = _s32(self.regs.get('capture_threshold', 0))
+            self.cfg.dirty.add('thr')
+        elif name == 'conv_phase_load_centers' and rising:
+            ic, qc = codecs.decode_center_register(_s32(self.regs.get('conv_phase_centers', 0)))
+            ch = value >> 1
+            self.cfg.ic[ch], self.cfg.qc[ch] = ic, qc
+            self.cfg.dirty.add('centers')
+        elif name in ('capture_Baseline_alpha', 'capture_base_Kf', 'capture_base_Kq',
+                      'capture_base_thresh', 'capture_base_mode'):
+            key = dict(capture_Baseline_alpha='alpha', capture_base_Kf='kf', capture_base_Kq='kq',
+                       capture_base_thresh='base_thr', capture_base_mode='mode')[name]
+            self.cfg.baseline[key] = value
+            self.cfg.dirty.add('baseline')
+        elif name == 'startBuffer':
+            self._buffering = bool(value)
+        elif name in ('startAccumulator', 'startSnap', 'startDAC', 'avgIQ_ctrl', 'snapPhase_ctrl',
+                      'snapqdr_ctrl', 'ch_we'):
+            pass  # control strobes: state is read back through self.regs
+        return None
+
+    def read_int(self, name):
+        if name == 'DRAM_LUT_rd_valid':
+            return 0                      # the device LUT is valid as soon as it is written
+        if name == 'pulses_addr':
+            self._advance_pulses()
+            return self._addr
+        if name not in self.regs:
+            raise RuntimeError('Request read_int failed: no register named %s' % name)
+        return self.regs[name]
+
+    def write(self, name, data, offset=0):
+        data = bytes(data)
+        if name == 'dram_memory':
+            I_dac, Q_dac, I_dds, Q_dds = codecs.unpack_luts(data)
+            self.cfg.dac_i, self.cfg.dac_q = I_dac, Q_dac
+            self.cfg.lut_i, self.cfg.lut_q = lut.deinterleave_dds(I_dds, Q_dds, self.C,
+                                                                  self.cfg.dds_lag)
+            self.cfg.dirty.add('dds')
+            self._t = 0
+            return None
+        m = FIR_RE.match(name)
+        if m:
+            if len(data) != 4:
+                raise RuntimeError('FIR register %s takes 4 bytes' % name)
+            self.regs[name] = data
+            return None
+        self.regs[name] = data
+        return None
+
+    def read(self, name, size, offset=0):
+        if name == 'avgIQ_bram':
+            return self._read_avgiq(size)
+        if name == 'snapPhase_bram':
+            return self._read_snap_phase(size)
+        if name in ('pulses_bram0', 'pulses_bram1'):
+            w0, w1 = codecs.reference_bram_words(self._ring)
+            w = w0 if name == 'pulses_bram0' else w1
+            return w.astype('>u4').tobytes()[offset:offset + size]
+        if name in self.regs and isinstance(self.regs[name], bytes):
+            return self.regs[name][offset:offset + size]
+        raise RuntimeError('Request read failed: no readable register named %s' % name)
+
+    # ---- device side -------------------------------------------------------------------------
+    def channelizer(self):
+        if self._chan is None:
+            if not self.gpu:
+                raise RuntimeError('FpgaClient(gpu=False) has no data path')
+            from .channelizer import Channelizer
+            self._chan = Channelizer(self.C, device=self.device, sample_rate=self.fs,
+                                     max_chunk=max(2 * self.N, 1 << 20))
+        return self._chan
+
+    def sync(self):
+        """Push dirty configuration groups to the device (one ABI call per group)."""
+        ch = self.channelizer()
+        d = self.cfg
+        if 'bins' in d.dirty:
+            ch.set_bins(d.bins)
+        if 'dds' in d.dirty:
+            ch.set_dds(d.lut_i, d.lut_q)
+        if 'fir' in d.dirty:
+            ch.set_fir(d.fir)
+        if 'thr' in d.dirty:
+            ch.set_thresholds(np.clip(d.thr, -(1 << 31), (1 << 31) - 1))
+        if 'centers' in d.dirty:
+            ch.set_centers(d.ic, d.qc)
+        if 'baseline' in d.dirty:
+            b = d.baseline
+            ch.set_baseline(b['mode'], b['alpha'], b['kf'], b['kq'], b['base_thr'])
+        d.dirty.clear()
+        return ch
+
+    def adc(self, n):
+        """Next n loop-back ADC samples: conj(DAC LUT) tiled (+ optional AWGN), int16 [n][2]."""
+        idx = (self._t + np.arange(n)) % lut.LUT_LEN
+        x = np.stack([self.cfg.dac_i[idx], -self.cfg.dac_q[idx]], axis=1).astype(np.float64)
+        if self.noise_sigma > 0:
+            x += self.rng.normal(0, self.noise_sigma, x.shape)
+        self._t += n
+        return np.clip(np.trunc(x), -32768, 32767).astype(np.int16)
+
+    def run(self, n_phase_samples):
+        """Stream enough loop-back ADC data for n phase samples per channel; returns
+        (phase [n][C], wide packets)."""
+        ch = self.sync()
+        return ch.process(self.adc(n_phase_samples * self.N))
+
+    def _read_avgiq(self, size):
+        ch = self.sync()
+        ch.process(self.adc(256 * self.N))       # accumulate over 256 phase samples
+        mi, mq = ch.avg_iq()
+        words = np.concatenate([np.rint(mi), np.rint(mq)]).astype('>i4')
+        return words.tobytes()[:size]
+
+    def _read_snap_phase(self, size):
+        nsamp = size // 2
+        phase, _ = self.run(nsamp)
+        ch = self.regs.get('ch_we', 0)
+        raw = np.clip(np.rint(phase[:, ch] * np.float32(8192)), -25736, 25736).astype(np.int64)
+        return codecs.encode_snap_phase(raw)[:size]
+
+    def _advance_pulses(self):
+        if not self._buffering:
+            return
+        _, ev = self.run(4096)
+        if len(ev) == 0:
+            return
+        ref = codecs.wide_to_reference(ev[codecs.unpack_wide(ev)['ch'] < 255])
+        for w in ref:
+            self._ring[self._addr] = w
+            self._addr = (self._addr + 1) % PULSE_RING
+
+
+def _s32(v):
+    v = int(v) & 0xFFFFFFFF
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+class RoachSetup:
+    """ROACH_Setup.py AppForm setup methods (GUI values as attributes)."""
+
+    def __init__(self, roach, dac_freqs, lo_freq, attens=None, sample_rate=512e6,
+                 n_channels=256, minimum_attenuation=0.0):
+        self.roach = roach
+        self.dac_freqs = list(dac_freqs)          # spinBox_DACfreq / textedit_DACfreqs
+        self.lo_freq = float(lo_freq)             # spinBox_loFreq
+        self.sampleRate = float(sample_rate)      # :82
+        self.freqRes = self.sampleRate / lut.LUT_LEN  # :83-84
+        self.n_channels = n_channels
+        self.attens = np.ones(max(n_channels, len(self.dac_freqs))) if attens is None else np.asarray(attens, float)
+        self.minimumAttenuation = minimum_attenuation
+        self.iq_centers = np.zeros(n_channels, complex)
+        self.dacStatus = 'off'
+
+    def freqCombLUT(self, echo, freq, sampleRate, resolution, amplitude=None, phase=None,
+                    random_phase='yes'):
+        I, Q, sf = lut.freq_comb_lut(echo, freq, sampleRate, resolution, amplitude, phase,
+                                     random_phase)
+        if echo == 'yes':
+            self.scale_factor = sf
+        return I, Q
+
+    def define_DAC_LUT(self):
+        self.I_dac, self.Q_dac, self.freqs_dac, self.scale_factor, _ = lut.define_dac_lut(
+            self.dac_freqs, self.lo_freq, self.attens[:len(self.dac_freqs)], self.sampleRate)
+
+    def define_DDS_LUT(self, phase=None):
+        d = lut.define_dds_lut(self.dac_freqs, self.lo_freq, self.n_channels, self.sampleRate,
+                               phase=phase, ch_shift=self.roach.cfg.dds_lag)
+        self.I_dds, self.Q_dds = d['I_dds'], d['Q_dds']
+        self.select_bins_written(d['bins'])
+        return d
+
+    def select_bins(self, readout_freqs):
+        bins, resid = lut.select_bins(readout_freqs, 2 * self.n_channels, self.sampleRate)
+        self.select_bins_written(bins)
+        return list(resid)
+
+    def select_bins_written(self, bins):
+        for i, b in enumerate(bins):               # ROACH_Setup.py:545-547
+            self.roach.write_int('bins', int(b))
+            self.roach.write_int('load_bins', (i << 1) + (1 << 0))
+            self.roach.write_int('load_bins', (i << 1) + (0 << 0))
+
+    def write_LUTs(self):
+        if self.dacStatus == 'off':
+            self.roach.write_int('startDAC', 0)
+        self.binaryData = codecs.pack_luts(self.I_dac, self.Q_dac, self.I_dds, self.Q_dds)
+        self.roach.write('dram_memory', self.binaryData)   # :570
+
+    def define_LUTs(self):
+        self.iq_centers = np.zeros(self.n_channels, complex)
+        self.define_DAC_LUT()
+        self.define_DDS_LUT()
+        self.write_LUTs()
+
+    def toggleDAC(self):
+        if self.dacStatus == 'off':
+            self.roach.write_int('startDAC', 1)
+            while self.roach.read_int('DRAM_LUT_rd_valid') != 0:   # :887-895
+                self.roach.write_int('startDAC', 0)
+                self.roach.write_int('startDAC', 1)
+            self.dacStatus = 'on'
+        else:
+            self.roach.write_int('startDAC', 0)
+            self.dacStatus = 'off'
+
+    def findIQcenters(self, I, Q):
+        return complex((np.max(I) + np.min(I)) / 2., (np.max(Q) + np.min(Q)) / 2.)
+
+    def loadIQcenters(self):
+        for ch in range(self.n_channels):          # :598-605
+            center = codecs.center_register(self.iq_centers[ch].real, self.iq_centers[ch].imag)
+            self.roach.write_int('conv_phase_centers', center)
+            self.roach.write_int('conv_phase_load_centers', (ch << 1) + (1 << 0))
+            self.roach.write_int('conv_phase_load_centers', 0)
+
+    def read_avg_iq(self):
+        self.roach.write_int('startAccumulator', 0)
+        self.roach.write_int('avgIQ_ctrl', 1)
+        self.roach.write_int('avgIQ_ctrl', 0)
+        self.roach.write_int('startAccumulator', 1)
+        data = self.roach.read('avgIQ_bram', 4 * 2 * self.n_channels)
+        v = np.frombuffer(data, '>i4').astype(np.float64)
+        return v[:self.n_channels], v[self.n_channels:]
+
+    def rotateLoopsReady(self):
+        """ROACH_Setup.py:645-671 for every tone channel: DDS phase = arctan2 of the on-resonance
+        average IQ (centre-subtracted), then redefine + rewrite the LUTs."""
+        I, Q = self.read_avg_iq()
+        phase = [0.] * self.n_channels
+        for n in range(len(self.dac_freqs)):
+            phase[n] = np.arctan2(Q[n] - self.iq_centers[n].imag, I[n] - self.iq_centers[n].real)
+        self.define_DDS_LUT(phase)
+        self.write_LUTs()
+        return phase
+
+
+class RoachPulses:
+    """ROACH_Pulses.py AppForm trigger-setup and readback methods."""
+
+    def __init__(self, roach, n_freqs, fir=None, n_channels=256):
+        self.roach = roach
+        self.N_freqs = n_freqs
+        self.n_channels = n_channels
+        self.fir = fir                               # importFIRcoeffs result (float taps)
+        self.zeroChannels = [0] * n_channels
+        self.thresholds = np.zeros(n_channels)
+        self.medians = np.zeros(n_channels)
+        self.customThresholds = np.full(n_channels, 360.)
+        self.scale_to_angle = codecs.SCALE_TO_ANGLE
+
+    def loadFIRcoeffs(self):
+        """ROACH_Pulses.py:59-111 (register writes of the 12-bit taps, deleted channels zero)."""
+        for ch in range(self.n_channels):
+            if ch < self.N_freqs and not self.zeroChannels[ch]:
+                taps = codecs.fir_quantise(self.fir)
+            else:
+                taps = np.zeros(26, np.int64)
+            for n, word in enumerate(codecs.fir_registers(taps)):
+                self.roach.write('FIR_b%db%d' % (2 * n, 2 * n + 1), word)
+                self.roach.write_int('FIR_load_coeff', (ch << 1) + (1 << 0))
+                self.roach.write_int('FIR_load_coeff', (ch << 1) + (0 << 0))
+
+    def snapshot_raw(self, ch, steps=10, L=2 ** 10):
+        data = b''
+        for _ in range(steps):                     # ROACH_Pulses.py:241-248
+            self.roach.write_int('ch_we', ch)
+            self.roach.write_int('startSnap', 0)
+            self.roach.write_int('snapPhase_ctrl', 1)
+            self.roach.write_int('snapPhase_ctrl', 0)
+            self.roach.write_int('startSnap', 1)
+            data += self.roach.read('snapPhase_bram', 4 * L)
+        return codecs.decode_snap_phase(data)
+
+    def loadSingleThreshold(self, ch, nsigma=2.5):
+        phase = self.snapshot_raw(ch)
+        threshold, med = codecs.threshold_from_phase(phase, nsigma)
+        self.thresholds[ch] = self.scale_to_angle * threshold
+        self.medians[ch] = self.scale_to_angle * med
+        if self.customThresholds[ch] != 360.0:
+            threshold = max(int(self.customThresholds[ch] / self.scale_to_angle), -25736)
+        self.roach.write_int('capture_threshold', threshold)
+        self.roach.write_int('capture_load_thresh', (ch << 1) + (1 << 0))
+        self.roach.write_int('capture_load_thresh', (ch << 1) + (0 << 0))
+        return threshold
+
+    def loadThresholds(self):
+        return [self.loadSingleThreshold(ch) for ch in range(self.N_freqs)]
+
+    def readPulses(self, steps=1):
+        """ROACH_Pulses.py:782-832: poll pulses_addr, decode the BRAM ring."""
+        self.roach.write_int('startBuffer', 1)
+        out = {}
+        for _ in range(steps):
+            addr0 = self.roach.read_int('pulses_addr')
+            addr1 = self.roach.read_int('pulses_addr')
+            b0 = self.roach.read('pulses_bram0', 4 * PULSE_RING)
+            b1 = self.roach.read('pulses_bram1', 4 * PULSE_RING)
+            rng = range(addr0, addr1) if addr1 >= addr0 else \
+                list(range(addr0, PULSE_RING)) + list(range(0, addr1))
+            for n in rng:
+                w1 = struct.unpack('>L', b1[4 * n:4 * n + 4])[0]
+                w0 = struct.unpack('>L', b0[4 * n:4 * n + 4])[0]
+                out.setdefault(w1 >> 24, []).append(dict(ts=w0 % 2 ** 20, base=(w0 >> 20) % 2 ** 12,
+                                                         peak=(w1 >> 12) % 2 ** 12,
+                                                         p1=w1 % 2 ** 12 - 2 ** 11))
+        self.roach.write_int('startBuffer', 0)
+        return out

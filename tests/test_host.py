@@ -1,0 +1,179 @@
+"""Host-side product code against the oracle restatement and the reference fixtures (CPU only):
+LUT synthesis, register codecs, the FpgaClient register shim and the ChannelizerControls
+mirror driving it (no GPU: the shim's data path is not touched)."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from mkids_sdr_amd import codecs, lut
+from mkids_sdr_amd.roach import FpgaClient, RoachPulses, RoachSetup
+from oracle import replay, setup_ref
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def test_lut_matches_reference_fixture():
+    d = np.load(os.path.join(GOLD, 'dac_lut.npz'))
+    I, Q, freqs, sf, _ = lut.define_dac_lut([4.1e9], 4.0e9, [1.0] * 256)
+    assert np.array_equal(I, d['I_dac']) and np.array_equal(Q, d['Q_dac'])
+    r = lut.define_dds_lut([4.1e9], 4.0e9, 256)
+    assert np.array_equal(r['I_dds'], d['I_dds']) and np.array_equal(r['Q_dds'], d['Q_dds'])
+
+
+@pytest.mark.parametrize('C,fs', [(64, 512e6), (256, 550e6), (1024, 550e6)])
+def test_lut_matches_oracle_multitone(C, fs):
+    rng = np.random.default_rng(C)
+    f = list(4e9 + rng.uniform(-fs / 2, fs / 2, min(C, 40)))
+    ph = rng.uniform(0, 2 * np.pi, C)
+    a = setup_ref.define_dds_lut(f, 4e9, C, 2 * C, fs, 154, phase=ph)
+    b = lut.define_dds_lut(f, 4e9, C, fs, phase=ph)
+    assert np.array_equal(a[0], b['I_dds']) and np.array_equal(a[1], b['Q_dds'])
+    assert list(a[2]) == list(b['bins'])
+    at = rng.uniform(0, 6, len(f))
+    A = setup_ref.define_dac_lut(f, 4e9, at, fs)
+    B = lut.define_dac_lut(f, 4e9, at, fs)
+    assert np.array_equal(A[0], B[0]) and np.array_equal(A[1], B[1]) and A[2] == B[2]
+
+
+def test_dds_interleave_roundtrip():
+    r = lut.define_dds_lut([4.1e9, 4.2e9], 4.0e9, 256, phase=np.linspace(0, 3, 256))
+    li, lq = lut.deinterleave_dds(r['I_dds'], r['Q_dds'], 256)
+    assert np.array_equal(li, r['lut_i']) and np.array_equal(lq, r['lut_q'])
+
+
+def test_pack_luts_matches_reference_packing():
+    d = np.load(os.path.join(GOLD, 'dac_lut.npz'))
+    n = 512  # the struct.pack loop is slow; a prefix pins the byte order
+    a = setup_ref.pack_luts(d['I_dac'][:n], d['Q_dac'][:n], d['I_dds'][:n], d['Q_dds'][:n])
+    b = codecs.pack_luts(d['I_dac'][:n], d['Q_dac'][:n], d['I_dds'][:n], d['Q_dds'][:n])
+    assert a == b
+    full = codecs.pack_luts(d['I_dac'], d['Q_dac'], d['I_dds'], d['Q_dds'])
+    assert len(full) == 512 * 1024
+    back = codecs.unpack_luts(full)
+    for x, k in zip(back, ('I_dac', 'Q_dac', 'I_dds', 'Q_dds')):
+        assert np.array_equal(x, d[k])
+
+
+def test_cast_bin_and_registers():
+    import json
+    g = json.load(open(os.path.join(GOLD, 'bin_vectors.json')))
+    for c in g['castBin']:
+        assert codecs.cast_bin(c['value'], c['nBits'], c['binaryPoint'], c['quantization']) == c['out']
+    r = codecs.baseline_registers()
+    assert r == dict(alpha=41, kf=82, kq=93623, base_thr=8192)
+    for p in g['peakfit']:
+        assert codecs.peakfit(*p['y']) == p['out']
+
+
+def test_fir_register_codec():
+    taps = codecs.fir_quantise(np.loadtxt(os.path.join(GOLD, 'fir', 'matched_30us.txt')))
+    words = codecs.fir_registers(taps)
+    assert words == setup_ref.fir_coeff_words(taps)
+    neg = np.array([-5, 7, -2048, 2047] + [0] * 22)
+    for n, w in enumerate(codecs.fir_registers(neg)):
+        assert codecs.decode_fir_register(w) == (neg[2 * n], neg[2 * n + 1])
+    zero_form = struct.pack('>h', 0) + struct.pack('>h', 0)       # ROACH_Pulses.py:104
+    assert codecs.decode_fir_register(zero_form) == (0, 0)
+
+
+@pytest.mark.parametrize('ic,qc', [(800.0, -24.0), (-8000.0, 16000.0), (-3.0, -9.0), (0.0, 0.0)])
+def test_center_register_codec(ic, qc):
+    w = codecs.center_register(ic, qc)
+    assert w == setup_ref.iq_center_register(ic, qc)
+    i2, q2 = codecs.decode_center_register(w)
+    assert i2 == 8 * int(ic / 8) and q2 == 8 * int(qc / 8)
+
+
+def test_threshold_codec_matches_oracle():
+    deg = np.loadtxt(os.path.join(GOLD, 'ch_snap_0.txt'))
+    raw = np.rint(deg / codecs.fix16_13_to_deg(1)).astype(np.int64)
+    assert codecs.threshold_from_phase(raw) == setup_ref.threshold_from_phase(raw)
+    block = np.stack([raw, raw[::-1], raw // 2], axis=1)
+    thr = codecs.thresholds_from_phase_block(block)
+    assert list(thr) == [setup_ref.threshold_from_phase(block[:, c])[0] for c in range(3)]
+
+
+def test_snapshot_codecs_match_reference_decoders():
+    rng = np.random.default_rng(1)
+    raw = rng.integers(-25736, 25737, 2048)
+    assert np.array_equal(setup_ref.snap_phase_decode(codecs.encode_snap_phase(raw)), raw)
+    assert np.array_equal(codecs.decode_snap_phase(codecs.encode_snap_phase(raw)), raw)
+    assert np.array_equal(setup_ref.conv_phase_snap_decode(codecs.encode_conv_phase_snap(raw)), raw)
+    I = rng.integers(-32768, 32768, 512)
+    Q = rng.integers(-32768, 32768, 512)
+    buf = codecs.encode_iq_snap(I, Q)
+    a, b = setup_ref.iq_snap_decode(buf)
+    assert np.array_equal(a, I) and np.array_equal(b, Q)
+    a, b = codecs.decode_iq_snap(buf)
+    assert np.array_equal(a, I) and np.array_equal(b, Q)
+
+
+def test_packet_codecs():
+    from oracle.trigger_ref import pack_wide
+    w = np.array([pack_wide(7, -3000, 1200, 123456789), pack_wide(200, 5000, -700, 17)], np.uint64)
+    u = codecs.unpack_wide(w)
+    assert list(u['ch']) == [7, 200]
+    ref = codecs.wide_to_reference(w)
+    b0, b1 = codecs.reference_bram_words(ref)
+    buf0 = b0.astype('>u4').tobytes() + bytes(4 * (2 ** 14 - 2))
+    buf1 = b1.astype('>u4').tobytes() + bytes(4 * (2 ** 14 - 2))
+    dec = setup_ref.decode_pulses(buf0, buf1, 0, 2)
+    assert dec[7][0][0] == 123456789 % 2 ** 20 and dec[7][0][2] == u['peak'][0]
+    assert dec[200][0][1] == u['base'][1]
+    with pytest.raises(ValueError):
+        codecs.wide_to_reference(np.array([pack_wide(300, 0, 0, 0)], np.uint64))
+
+
+def test_register_shim_decodes_setup_path():
+    """RoachSetup/RoachPulses drive the FpgaClient exactly like the reference; the shim's decoded
+    device configuration must equal the direct computation."""
+    C = 256
+    roach = FpgaClient(n_channels=C, gpu=False)
+    roach.progdev('pulse_trigger_2022_Jan_24_1322.bof')
+    freqs = [4.0e9 + d for d in (-91.3e6, 12.5e6, 100e6, 203.1e6)]
+    rs = RoachSetup(roach, freqs, 4.0e9, n_channels=C)
+    rs.define_LUTs()
+    d = lut.define_dds_lut(freqs, 4.0e9, C)
+    assert np.array_equal(roach.cfg.bins, d['bins'] % (2 * C))
+    assert np.array_equal(roach.cfg.lut_i, d['lut_i']) and np.array_equal(roach.cfg.lut_q, d['lut_q'])
+    I, Q, _, _, _ = lut.define_dac_lut(freqs, 4.0e9, np.ones(4))
+    assert np.array_equal(roach.cfg.dac_i, I) and np.array_equal(roach.cfg.dac_q, Q)
+    rs.iq_centers[:4] = [800 - 24j, -8000 + 16000j, -3 - 9j, 1000 + 1000j]
+    rs.loadIQcenters()
+    assert roach.cfg.ic[1] == -8000.0 and roach.cfg.qc[1] == 16000.0 and roach.cfg.qc[0] == -24.0
+    fir = np.loadtxt(os.path.join(GOLD, 'fir', 'matched_30us.txt'))
+    rp = RoachPulses(roach, 4, fir, n_channels=C)
+    rp.zeroChannels[2] = 1
+    rp.loadFIRcoeffs()
+    q = codecs.fir_quantise(fir)
+    assert np.array_equal(roach.cfg.fir[0], q) and np.array_equal(roach.cfg.fir[3], q)
+    assert not roach.cfg.fir[2].any() and not roach.cfg.fir[4:].any()
+    for ch, thr in ((0, -5913), (3, -120)):
+        roach.write_int('capture_threshold', thr)
+        roach.write_int('capture_load_thresh', (ch << 1) + 1)
+        roach.write_int('capture_load_thresh', ch << 1)
+    assert roach.cfg.thr[0] == -5913 and roach.cfg.thr[3] == -120
+    roach.write_int('capture_Baseline_alpha', 41)
+    roach.write_int('capture_base_Kf', 82)
+    assert roach.cfg.baseline['kf'] == 82
+    with pytest.raises(RuntimeError):
+        roach.read_int('no_such_register')
+    assert roach.read_int('DRAM_LUT_rd_valid') == 0
+
+
+def test_replay_triggers_restated():
+    """Host replays (pulse_triggering*.py) on a synthetic phase trace: hits at the injected
+    pulses, skip semantics as in the reference loops."""
+    rng = np.random.default_rng(5)
+    x = rng.normal(10.0, 1.0, 20000)
+    starts = [3000, 3500, 9000, 15000]
+    for s in starts:
+        t = np.arange(600)
+        x[s:s + 600] -= 60 * np.exp(-t / 65.0)
+    h = replay.rolling_mean_trigger(x)
+    assert h == [3000, 9000, 15000]   # 3500 falls inside the 1000-sample skip after 3000
+    h2 = replay.block_mean_trigger(x, averagelength=128, start=100, need=300, skip=200,
+                                   wrap_negative=False)
+    assert h2[0] == 3000 and 3500 in h2

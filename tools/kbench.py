@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of libmkidgpu build variants in ONE process (cdna guide §5.4 rule 24).
+
+    python tools/kbench.py [--log2-samples 28] [--rounds 5] variantA.so variantB.so ...
+Each variant gets its own context on the same synthetic 1024-channel input (bench.py's feedline,
+calibrated); per round every variant processes the input once; per-kernel HIP-event times are
+reported as median / min over rounds.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('libs', nargs='+')
+    ap.add_argument('--log2-samples', type=int, default=28)
+    ap.add_argument('--rounds', type=int, default=5)
+    ap.add_argument('--channels', type=int, default=1024)
+    args = ap.parse_args()
+    import torch
+    import bench
+    from mkids_sdr_amd import codecs, lut
+    from mkids_sdr_amd.channelizer import Channelizer
+
+    C = args.channels
+    N = 2 * C
+    S = 1 << args.log2_samples
+    J = S // N
+    fs = 550e6
+    dev = torch.device('cuda', 0)
+    feed = bench.setup_feedline(C, fs, 1000)
+    mf = codecs.fir_quantise(np.loadtxt(os.path.join(ROOT, 'tests/golden/fir/matched_30us.txt')))
+    lpf = codecs.fir_quantise(np.loadtxt(os.path.join(ROOT, 'tests/golden/fir/BlackmanFilter_250kHz.txt')))
+    base = torch.from_numpy(feed['base']).to(dev)
+    tones = np.zeros(C, dtype=[('amp', '<f4'), ('phase0', '<f4'), ('freq_index', '<i4'), ('pad', '<i4')])
+    tones['amp'] = feed['tone_amp']
+    tones['phase0'] = -np.asarray(feed['phases'])
+    tones['freq_index'] = feed['freq_index']
+    d_tones = torch.from_numpy(tones.view(np.uint8)).to(dev)
+    rng = np.random.default_rng(42)
+    ps, pt, pa = bench.make_pulses(C, S, N, 1.0 / 2048, rng)
+    pul = np.zeros(len(ps), dtype=[('start', '<i8'), ('tone', '<i4'), ('amp_rad', '<f4')])
+    pul['start'], pul['tone'], pul['amp_rad'] = ps, pt, pa
+    d_pul = torch.from_numpy(pul.view(np.uint8)).to(dev)
+    x = torch.empty(S * 2, dtype=torch.int16, device=dev)
+    sigma = 0.01 * 32767 / np.sqrt(2.0)
+    phase = torch.empty(J * C, dtype=torch.float32, device=dev)
+    cap = J * C // 8 + 1024
+    d_ev = torch.empty(cap, dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+
+    chans = []
+    for i, path in enumerate(args.libs):
+        ch = Channelizer(C, max_chunk=S, sample_rate=fs, lib_path=os.path.abspath(path))
+        ch.set_bins(feed['dds']['bins'])
+        ch.set_lpf(lpf)
+        ch.set_fir(np.tile(mf, (C, 1)))
+        if i == 0:
+            ch.synth_adc(x, S, 0, base, d_tones, d_pul, len(ps), 0.1 * N, 65.0 * N, 390 * N, sigma, 42)
+            ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
+            ch.set_thresholds(np.full(C, -(1 << 30), np.int32))
+            ch.process_device(x, S, phase, d_ev, cap, d_cnt)
+            torch.cuda.synchronize()
+            mi, mq = ch.avg_iq()
+            dds = lut.define_dds_lut(feed['f_rf'], feed['f_base'], C, fs, phase=np.arctan2(mq, mi))
+        ch.set_dds(dds['lut_i'], dds['lut_q'])
+        ch.set_thresholds(np.full(C, -3000, np.int32))
+        chans.append(ch)
+    times = {p: {} for p in args.libs}
+    for r in range(args.rounds + 1):
+        for path, ch in zip(args.libs, chans):
+            ch.reset()
+            ch.set_timing(True)
+            ch.process_device(x, S, phase, d_ev, cap, d_cnt)
+            torch.cuda.synchronize()
+            t = ch.timing()
+            ch.set_timing(False)
+            if r == 0:
+                continue  # warm-up round
+            for k, (ms, n) in t.items():
+                times[path].setdefault(k, []).append(ms)
+    out = {}
+    for path in args.libs:
+        out[os.path.basename(path)] = {k: dict(median=float(np.median(v)), min=float(np.min(v)))
+                                       for k, v in times[path].items()}
+    print(json.dumps(dict(samples=S, channels=C, rounds=args.rounds, kernels_ms=out), indent=1))
+
+
+if __name__ == '__main__':
+    main()

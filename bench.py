@@ -197,7 +197,10 @@ def main():
         kt = {k: (v[0] / max(v[1], 1)) for k, v in timing.items()}
         dom = max(kt, key=kt.get)
         n_launch = timing[dom][1] // args.steps if timing[dom][1] else 1
-        alg = {'k_channelize': 4.0, 'k_lpf_phase': 0.0 if args.no_phase else 2.0,
+        # algorithmic HBM bytes per ADC sample of each kernel (DESIGN.md "Kernels"): the fused
+        # front end reads 4 B of I/Q and writes 1 B of raw phase (+2 B of float phase)
+        alg = {'k_front': 5.0 + (0.0 if args.no_phase else 2.0),
+               'k_channelize': 4.0, 'k_lpf_phase': 1.0 + (0.0 if args.no_phase else 2.0),
                'k_trigger': 0.0, 'k_compact': 0.0}
         per_launch_samples = S / max(n_launch, 1)
         a_bytes = alg.get(dom, 0.0) * per_launch_samples
@@ -206,7 +209,8 @@ def main():
         prof = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
         if os.path.exists(prof):
             try:
-                traffic = json.load(open(prof)).get(dom, {}).get('hbm_bytes_per_launch')
+                bps = json.load(open(prof)).get(dom, {}).get('hbm_bytes_per_sample')
+                traffic = None if bps is None else round(bps * per_launch_samples)
             except Exception:
                 traffic = None
         fft_flops = 5.0 * N * np.log2(N) / (N / 2)      # per input sample (hop N/2)

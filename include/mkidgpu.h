@@ -53,6 +53,11 @@ extern "C" {
 #define MKID_PKT_BASE_SHIFT 28
 #define MKID_PKT_TS_MASK ((1ull << 28) - 1)
 
+/* Front-end (K1-K6) execution: one fused kernel (z stays on-chip) or two kernels with the complex
+ * baseband z staged in HBM. Results agree to float rounding; AUTO picks fused where supported. */
+#define MKID_FRONT_AUTO 0
+#define MKID_FRONT_SPLIT 1
+
 typedef struct mkid_ctx mkid_ctx;
 
 typedef struct mkid_cfg {
@@ -63,7 +68,8 @@ typedef struct mkid_cfg {
     int32_t dds_entries;       /* P = 2^16 / C LO samples per channel; ROACH_Setup.py:521-530 */
     int32_t dead_time;         /* trigger dead time in phase samples (build decision)         */
     int32_t max_events_per_ch; /* per-call event capacity per channel (0 = derive from chunk) */
-    int32_t reserved;
+    int32_t front;             /* MKID_FRONT_AUTO (fused K1-K6 kernel where N <= 2048) or
+                                  MKID_FRONT_SPLIT (channeliser + low-pass kernels, z in HBM)  */
     int64_t max_chunk;         /* largest nsamples per process call (workspace sizing)        */
     double sample_rate;        /* fs, complex S/s; ROACH_Setup.py:82                           */
 } mkid_cfg;
@@ -154,7 +160,8 @@ int mkid_pack_reference(const uint64_t* wide, int64_t n, uint64_t* out);
 #define MKID_K_FIR_PHASE 1
 #define MKID_K_TRIGGER 2
 #define MKID_K_COMPACT 3
-#define MKID_K_COUNT 4
+#define MKID_K_FRONT 4        /* fused K1-K6 (replaces CHANNELIZE + FIR_PHASE when used) */
+#define MKID_K_COUNT 5
 int mkid_set_timing(mkid_ctx* ctx, int32_t enable);
 int mkid_get_timing(mkid_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches);
 const char* mkid_kernel_name(int32_t kernel);

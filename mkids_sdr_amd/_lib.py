@@ -18,7 +18,8 @@ MKID_E_OVERFLOW = -4
 MKID_E_NODEV = -5
 
 BASE_NONE, BASE_EMA, BASE_SVF = 0, 1, 2
-K_CHANNELIZE, K_FIR_PHASE, K_TRIGGER, K_COMPACT, K_COUNT = 0, 1, 2, 3, 4
+K_CHANNELIZE, K_FIR_PHASE, K_TRIGGER, K_COMPACT, K_FRONT, K_COUNT = 0, 1, 2, 3, 4, 5
+FRONT_AUTO, FRONT_SPLIT = 0, 1
 
 PKT_CH_SHIFT, PKT_PEAK_SHIFT, PKT_BASE_SHIFT = 52, 40, 28
 PKT_TS_MASK = (1 << 28) - 1
@@ -37,7 +38,7 @@ class Cfg(ctypes.Structure):
     _fields_ = [('n_channels', ctypes.c_int32), ('fft_len', ctypes.c_int32),
                 ('pfb_taps', ctypes.c_int32), ('fir_taps', ctypes.c_int32),
                 ('dds_entries', ctypes.c_int32), ('dead_time', ctypes.c_int32),
-                ('max_events_per_ch', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('max_events_per_ch', ctypes.c_int32), ('front', ctypes.c_int32),
                 ('max_chunk', ctypes.c_int64), ('sample_rate', ctypes.c_double)]
 
 

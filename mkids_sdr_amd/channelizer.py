@@ -26,7 +26,7 @@ def _ptr(a):
 
 class Channelizer:
     def __init__(self, n_channels, device=0, max_chunk=1 << 22, dead_time=32, sample_rate=512e6,
-                 max_events_per_ch=0, lib_path=None):
+                 max_events_per_ch=0, lib_path=None, front='auto'):
         self._L = _lib.load(lib_path)
         cfg = _lib.Cfg()
         _lib.check(self._L.mkid_default_cfg(ctypes.byref(cfg), int(n_channels)))
@@ -34,6 +34,9 @@ class Channelizer:
         cfg.dead_time = int(dead_time)
         cfg.sample_rate = float(sample_rate)
         cfg.max_events_per_ch = int(max_events_per_ch)
+        if front not in ('auto', 'split'):
+            raise ValueError("front must be 'auto' (fused K1-K6 where supported) or 'split'")
+        cfg.front = _lib.FRONT_AUTO if front == 'auto' else _lib.FRONT_SPLIT
         h = ctypes.c_void_p()
         _lib.check(self._L.mkid_create(ctypes.byref(cfg), int(device), ctypes.byref(h)))
         self._h = h

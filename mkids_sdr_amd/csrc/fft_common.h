@@ -87,13 +87,26 @@ template <int N>
 constexpr int lds_frame_elems() { return N + N / 16; }
 
 // Stockham pass pieces; thread t of NT = N/PTS threads holds PTS points = PTS/R butterflies.
+// Every LDS address is one per-thread base + a compile-time offset (lpad(i + 16k) = lpad(i) +
+// 17k), so the compiler keeps one address VGPR per butterfly instead of one per point.
 template <int N, int PTS, int R>
 __device__ __forceinline__ void st_read(const float2* buf, float2 (&v)[PTS], int t) {
     constexpr int NT = N / PTS, NB = PTS / R, NR = N / R;
+    static_assert(NT % 16 == 0 && NR % 16 == 0, "pad-linear offsets");
+    const float2* b = buf + lpad(t);
 #pragma unroll
     for (int q = 0; q < NB; ++q)
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[q * R + r] = buf[lpad(t + q * NT + r * NR)];
+        for (int r = 0; r < R; ++r) v[q * R + r] = b[(q * NT + r * NR) / 16 * 17];
+}
+
+// lpad(base + r NS) - lpad(base) for the bases a Stockham write produces (base mod 16 < 8 when
+// NS == 8 and NS R >= 16; base mod 16 in {0, 4, 8, 12} when NS == 1).
+template <int NS, int R>
+__device__ __forceinline__ constexpr int st_woff(int r) {
+    static_assert(NS % 16 == 0 || (NS == 8 && NS * R >= 16) || (NS == 1 && R <= 8 && R % 4 == 0),
+                  "pad-linear write offsets");
+    return NS % 16 == 0 ? r * NS / 16 * 17 : (NS == 8 ? 8 * r + (r >> 1) : r);
 }
 
 template <int N, int PTS, int R, int NS>
@@ -102,9 +115,9 @@ __device__ __forceinline__ void st_write(float2* buf, const float2 (&v)[PTS], in
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
         const int j = t + q * NT;
-        const int base = (j / NS) * NS * R + (j % NS);
+        float2* b = buf + lpad((j / NS) * NS * R + (j % NS));
 #pragma unroll
-        for (int r = 0; r < R; ++r) buf[lpad(base + r * NS)] = v[q * R + r];
+        for (int r = 0; r < R; ++r) b[st_woff<NS, R>(r)] = v[q * R + r];
     }
 }
 
@@ -140,13 +153,60 @@ struct Twiddle {
     }
 };
 
+// Register-lean twiddles: one base w = exp(-2 pi i (j%NS) / (NS R)) per butterfly; the powers
+// w^2..w^(R-1) are rebuilt by at most 6 complex multiplies per radix-8 butterfly (error a few ulp,
+// far below the 1e-5 rad phase bar) instead of holding R-1 complex values in VGPRs.
+template <int N, int PTS, int R, int NS>
+struct TwiddleRec {
+    static constexpr int NB = PTS / R;
+    float2 w[NB];
+    __device__ __forceinline__ void init(int t) {
+        constexpr int NT = N / PTS;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int m = (t + q * NT) % NS;
+            double s, c;
+            sincospi(-2.0 * (double)m / (double)(NS * R), &s, &c);
+            w[q] = make_float2((float)c, (float)s);
+        }
+    }
+    __device__ __forceinline__ void apply(float2 (&v)[PTS]) const {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            float2* b = &v[q * R];
+            float2 w1 = w[q];
+            // opaque to the optimiser: otherwise loop-invariant code motion hoists the powers
+            // out of the frame loop and they occupy registers again
+            asm volatile("" : "+v"(w1.x), "+v"(w1.y));
+            if constexpr (R == 2) {
+                b[1] = cmul(b[1], w1);
+            } else if constexpr (R == 4) {
+                const float2 w2 = cmul(w1, w1);
+                b[1] = cmul(b[1], w1);
+                b[2] = cmul(b[2], w2);
+                b[3] = cmul(b[3], cmul(w2, w1));
+            } else {
+                static_assert(R == 8, "radix");
+                const float2 w2 = cmul(w1, w1), w4 = cmul(w2, w2), w3 = cmul(w2, w1);
+                b[1] = cmul(b[1], w1);
+                b[2] = cmul(b[2], w2);
+                b[3] = cmul(b[3], w3);
+                b[4] = cmul(b[4], w4);
+                b[5] = cmul(b[5], cmul(w4, w1));
+                b[6] = cmul(b[6], cmul(w4, w2));
+                b[7] = cmul(b[7], cmul(w4, w3));
+            }
+        }
+    }
+};
+
 template <int N>
-struct Plan;
-template <> struct Plan<128>  { static constexpr int PTS = 16, NP = 2, R1 = 16, R2 = 8,  R3 = 1; };
-template <> struct Plan<256>  { static constexpr int PTS = 16, NP = 2, R1 = 16, R2 = 16, R3 = 1; };
-template <> struct Plan<512>  { static constexpr int PTS = 8,  NP = 3, R1 = 8,  R2 = 8,  R3 = 8; };
-template <> struct Plan<1024> { static constexpr int PTS = 16, NP = 3, R1 = 16, R2 = 16, R3 = 4; };
-template <> struct Plan<2048> { static constexpr int PTS = 16, NP = 3, R1 = 16, R2 = 16, R3 = 8; };
-template <> struct Plan<4096> { static constexpr int PTS = 16, NP = 3, R1 = 16, R2 = 16, R3 = 16; };
+struct Plan8;  // PTS = 8 points per thread; radix sequence R1..R4 (1 = no pass)
+template <> struct Plan8<128>  { static constexpr int NP = 3, R[4] = {8, 4, 4, 1}; };
+template <> struct Plan8<256>  { static constexpr int NP = 3, R[4] = {8, 8, 4, 1}; };
+template <> struct Plan8<512>  { static constexpr int NP = 3, R[4] = {8, 8, 8, 1}; };
+template <> struct Plan8<1024> { static constexpr int NP = 4, R[4] = {8, 8, 4, 4}; };
+template <> struct Plan8<2048> { static constexpr int NP = 4, R[4] = {8, 8, 8, 4}; };
+template <> struct Plan8<4096> { static constexpr int NP = 4, R[4] = {8, 8, 8, 8}; };
 
 }  // namespace mkid

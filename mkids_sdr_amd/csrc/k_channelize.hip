@@ -6,24 +6,24 @@
 //          new hops with ONE 16-byte global load per thread, issued one iteration ahead so its
 //          latency hides behind the FFT; each sample is read from HBM once (+ (2T-1)/run warm-up).
 //   PFB    u[p] = sum_tau h[tau N + p] x[(k+1)M - TN + tau N + p]  (h in registers, x from LDS)
-//   FFT    Stockham radix-8/4 passes, butterflies in registers, twiddles in registers, exchanges
-//          through padded LDS
-//   K3/4   z[k][c] = X[bin_c] (-1)^(bin_c (k+1)) conj(LUT_c[k mod P]) / 2^15, coalesced stores
+//   FFT    Stockham radix-8/4 passes, butterflies in registers, one twiddle base per butterfly
+//          (powers rebuilt in registers), exchanges through padded LDS. With MKID_CHAN_DBUF the
+//          passes ping-pong between two LDS buffers: one barrier per pass instead of two.
+//   K3/4   z[k][c] = X[bin_c] (-1)^(bin_c (k+1)) conj(LUT_c[k mod P]) / 2^15; LO table [P][C] so
+//          both the LO row and the z row of a frame are contiguous (coalesced)
 // Reference geometry: fft_len/channels ROACH_Setup.py:507,515; bins ROACH_Setup.py:534-550; DDS
 // LUT at 2 fs/N ROACH_Setup.py:525. Taps/window of the PFB: build decision (firmware absent).
 #include "fft_common.h"
 #include "mkid_internal.h"
 
-namespace mkid {
+#ifndef MKID_CHAN_MINWAVES
+#define MKID_CHAN_MINWAVES 1
+#endif
+#ifndef MKID_CHAN_DBUF
+#define MKID_CHAN_DBUF 1
+#endif
 
-template <int N>
-struct Plan8;  // PTS = 8 points per thread; radix sequence R1..R4 (1 = no pass)
-template <> struct Plan8<128>  { static constexpr int NP = 3, R[4] = {8, 4, 4, 1}; };
-template <> struct Plan8<256>  { static constexpr int NP = 3, R[4] = {8, 8, 4, 1}; };
-template <> struct Plan8<512>  { static constexpr int NP = 3, R[4] = {8, 8, 8, 1}; };
-template <> struct Plan8<1024> { static constexpr int NP = 4, R[4] = {8, 8, 4, 4}; };
-template <> struct Plan8<2048> { static constexpr int NP = 4, R[4] = {8, 8, 8, 4}; };
-template <> struct Plan8<4096> { static constexpr int NP = 4, R[4] = {8, 8, 8, 8}; };
+namespace mkid {
 
 constexpr int kPts = 8;
 
@@ -35,29 +35,27 @@ struct Geo {
     static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
     static constexpr int RS = 2 * T - 1 + FPB;          // ring slots (hops)
     static constexpr int LDSF = lds_frame_elems<N>();
+    static constexpr int NBUF = MKID_CHAN_DBUF ? 2 : 1;  // FFT exchange buffers per frame
     static constexpr int CPT = C / NT;                  // channels per thread in select
     static constexpr int NEW = FPB * M;                 // new samples per iteration
     static constexpr int SPT = NEW / BT;                // new samples per thread (4)
     static_assert(SPT == 4, "one 16-byte load per thread per iteration");
     static constexpr int NS2 = Plan8<N>::R[0], NS3 = NS2 * Plan8<N>::R[1], NS4 = NS3 * Plan8<N>::R[2];
-    static constexpr size_t lds_bytes = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8;
+    static constexpr size_t lds_bytes = (size_t)RS * M * 4 + (size_t)FPB * NBUF * LDSF * 8;
 };
 
-// Load the 16 bytes (4 samples) this thread contributes to hop-group `it` of the run.
+// Load the 16 bytes (4 samples) this thread contributes to the FPB hops starting at first_hop.
 template <int N>
 __device__ __forceinline__ uint4 load_new(const ChanArgs& a, int64_t first_hop, int tid) {
     using G = Geo<N>;
     const int64_t s0 = first_hop * G::M + (int64_t)tid * G::SPT;  // sample index in chunk
     if (s0 >= (int64_t)a.K * G::M) return make_uint4(0, 0, 0, 0);
-    if (s0 >= 0) return *reinterpret_cast<const uint4*>(a.x + s0);
-    const int64_t hs = s0 + (G::T * N - G::M);  // into xhist (H = TN - M samples)
+    if (s0 >= -a.avail) return *reinterpret_cast<const uint4*>(a.x + s0);
+    const int64_t hs = s0 + a.avail + (G::T * N - G::M);  // into xhist (H = TN - M samples)
     return *reinterpret_cast<const uint4*>(a.xhist + hs);
 }
 
 template <int N>
-#ifndef MKID_CHAN_MINWAVES
-#define MKID_CHAN_MINWAVES 1
-#endif
 __global__ __launch_bounds__(Geo<N>::BT, MKID_CHAN_MINWAVES) void k_channelize(ChanArgs a) {
     using G = Geo<N>;
     using PL = Plan8<N>;
@@ -69,7 +67,8 @@ __global__ __launch_bounds__(Geo<N>::BT, MKID_CHAN_MINWAVES) void k_channelize(C
     const int tid = threadIdx.x;
     const int slot = tid / NT;
     const int t = tid % NT;
-    float2* buf = fbuf + slot * G::LDSF;
+    float2* bufA = fbuf + slot * G::NBUF * G::LDSF;
+    [[maybe_unused]] float2* bufB = bufA + (G::NBUF - 1) * G::LDSF;  // == bufA without double buffering
 
     // PFB taps for this thread's points (constant over frames)
     float h[T][PTS];
@@ -78,11 +77,11 @@ __global__ __launch_bounds__(Geo<N>::BT, MKID_CHAN_MINWAVES) void k_channelize(C
 #pragma unroll
         for (int r = 0; r < PTS; ++r) h[tau][r] = a.pfb[tau * N + t + r * NT];
 
-    Twiddle<N, PTS, PL::R[1], G::NS2> tw2;
+    TwiddleRec<N, PTS, PL::R[1], G::NS2> tw2;
     tw2.init(t);
-    Twiddle<N, PTS, PL::R[2], G::NS3> tw3;
+    TwiddleRec<N, PTS, PL::R[2], G::NS3> tw3;
     tw3.init(t);
-    Twiddle<N, PTS, (PL::NP == 4 ? PL::R[3] : 2), G::NS4> tw4;
+    TwiddleRec<N, PTS, (PL::NP == 4 ? PL::R[3] : 2), G::NS4> tw4;
     if constexpr (PL::NP == 4) tw4.init(t);
 
     int32_t bin[G::CPT];
@@ -130,36 +129,65 @@ __global__ __launch_bounds__(Geo<N>::BT, MKID_CHAN_MINWAVES) void k_channelize(C
             v[r] = make_float2(ur, ui);
         }
         st_dft<PTS, PL::R[0]>(v);
-        __syncthreads();  // all PFB reads of the oldest FPB hops are done
-        {   // refill the ring with the prefetched hops, start the next prefetch
+#if MKID_CHAN_DBUF
+        // pass 1 -> A. The barrier publishes A and retires every ring read of this iteration.
+        st_write<N, PTS, PL::R[0], 1>(bufA, v, t);
+        __syncthreads();
+        {
             const int64_t hop = kb + G::FPB + (tid * G::SPT) / M;
-            const int off = (tid * G::SPT) % M;
-            *reinterpret_cast<uint4*>(ring + (int)(hop % RS) * M + off) = pre;
+            *reinterpret_cast<uint4*>(ring + (int)(hop % RS) * M + (tid * G::SPT) % M) = pre;
             pre = load_new<N>(a, kb + 2 * G::FPB, tid);
         }
-        // ---- FFT ----
-        st_write<N, PTS, PL::R[0], 1>(buf, v, t);
+        st_read<N, PTS, PL::R[1]>(bufA, v, t);
+        tw2.apply(v);
+        st_dft<PTS, PL::R[1]>(v);
+        st_write<N, PTS, PL::R[1], G::NS2>(bufB, v, t);
         __syncthreads();
-        st_read<N, PTS, PL::R[1]>(buf, v, t);
+        st_read<N, PTS, PL::R[2]>(bufB, v, t);
+        tw3.apply(v);
+        st_dft<PTS, PL::R[2]>(v);
+        st_write<N, PTS, PL::R[2], G::NS3>(bufA, v, t);
+        __syncthreads();
+        const float2* fin = bufA;
+        if constexpr (PL::NP == 4) {
+            st_read<N, PTS, PL::R[3]>(bufA, v, t);
+            tw4.apply(v);
+            st_dft<PTS, PL::R[3]>(v);
+            st_write<N, PTS, PL::R[3], G::NS4>(bufB, v, t);
+            __syncthreads();
+            fin = bufB;
+        }
+#else
+        __syncthreads();  // all PFB reads of the oldest FPB hops are done
+        {
+            const int64_t hop = kb + G::FPB + (tid * G::SPT) / M;
+            *reinterpret_cast<uint4*>(ring + (int)(hop % RS) * M + (tid * G::SPT) % M) = pre;
+            pre = load_new<N>(a, kb + 2 * G::FPB, tid);
+        }
+        st_write<N, PTS, PL::R[0], 1>(bufA, v, t);
+        __syncthreads();
+        st_read<N, PTS, PL::R[1]>(bufA, v, t);
         __syncthreads();
         tw2.apply(v);
         st_dft<PTS, PL::R[1]>(v);
-        st_write<N, PTS, PL::R[1], G::NS2>(buf, v, t);
+        st_write<N, PTS, PL::R[1], G::NS2>(bufA, v, t);
         __syncthreads();
-        st_read<N, PTS, PL::R[2]>(buf, v, t);
+        st_read<N, PTS, PL::R[2]>(bufA, v, t);
         __syncthreads();
         tw3.apply(v);
         st_dft<PTS, PL::R[2]>(v);
-        st_write<N, PTS, PL::R[2], G::NS3>(buf, v, t);
+        st_write<N, PTS, PL::R[2], G::NS3>(bufA, v, t);
         __syncthreads();
         if constexpr (PL::NP == 4) {
-            st_read<N, PTS, PL::R[3]>(buf, v, t);
+            st_read<N, PTS, PL::R[3]>(bufA, v, t);
             __syncthreads();
             tw4.apply(v);
             st_dft<PTS, PL::R[3]>(v);
-            st_write<N, PTS, PL::R[3], G::NS4>(buf, v, t);
+            st_write<N, PTS, PL::R[3], G::NS4>(bufA, v, t);
             __syncthreads();
         }
+        const float2* fin = bufA;
+#endif
         // ---- bin select + DDC ----
         if (k < k_end) {
             const int64_t kg = a.k0 + k;
@@ -168,13 +196,16 @@ __global__ __launch_bounds__(Geo<N>::BT, MKID_CHAN_MINWAVES) void k_channelize(C
 #pragma unroll
             for (int q = 0; q < G::CPT; ++q) {
                 const int c = t + q * NT;
-                float2 X = buf[lpad(bin[q])];
+                float2 X = fin[lpad(bin[q])];
                 if (podd & bin[q] & 1) X = make_float2(-X.x, -X.y);
-                const float2 lo = a.lo[(int64_t)c * a.P + lidx];
+                const float2 lo = a.lo[lidx * C + c];
                 a.z[k * C + c] = cmul(X, lo);
             }
         }
-        // the next iteration's first LDS write (ring refill) happens after its own barrier
+        // Double-buffered: the next iteration's first LDS write goes to A before any barrier.
+        // With 4 passes the select above read B (safe); with 3 it read A: barrier first. (Single
+        // buffer: the next write follows the post-PFB barrier.)
+        if constexpr (MKID_CHAN_DBUF && PL::NP != 4) __syncthreads();
     }
 }
 

@@ -1,0 +1,249 @@
+// Fused front end, K1-K6 in one pass over the ADC stream: polyphase filter bank + N-point FFT
+// (2x oversampled, hop M = N/2) + bin select + DDC + 26-tap IQ low-pass decimating by 2 +
+// IQ-centre subtraction + atan2 + Fix16_13. The complex baseband z never leaves the CU: HBM sees
+// 4 B/sample of int16 I/Q in and 1 B/sample of raw phase (+2 B/sample float phase) out.
+//
+// A workgroup of BT = N/2 = C threads owns a contiguous run of frames [k_b, k_e) and walks it
+// FPB = 4 frames per iteration (NT = N/8 threads per frame, 8 points per thread):
+//   input  LDS ring of RS = 2T-1+FPB hops of M int16 I/Q samples; each iteration brings 4 new
+//          hops with ONE 16-byte global load per thread, issued one iteration ahead.
+//   PFB    u[p] = sum_tau h[tau N + p] x[(k+1)M - TN + tau N + p]   (h as float4 per p in LDS)
+//   FFT    Stockham radix-8/4 passes through a padded per-frame LDS buffer (fft_common.h).
+//   DDC    thread c = channel c: z_k = X_k[bin_c] (-1)^(bin_c (k+1)) conj(LUT_c[k mod P]) / 2^15
+//          for the 4 frames of the iteration (LO table [P][C]: one contiguous row per frame).
+//   LPF    transposed form, 13 complex accumulators per thread: frame 2j adds g_{2m+1} z to
+//          output j+m, frame 2j+1 adds g_{2m} z and completes output j:
+//          y_j = sum_i g_i z_{2j+1-i}      (taps int(lpf*(2**11-1))/2^11, ROACH_Pulses.py:69,88)
+//   phase  phi_j = atan2(Im y - qc, Re y - ic)     (pulse_triggering_IQ.py:152)
+//          raw_j = clamp(rint(phi_j 2^13), +-25736) (Fix16_13, ROACH_Pulses.py:274-278)
+// Each run starts kLpfHist = 24 frames early (warm-up: the low-pass history is recomputed from
+// the ADC samples instead of being stored), so frames before the chunk come from an ADC history
+// of (2T-1+24) hops carried between calls. Reference geometry: ROACH_Setup.py:507-550.
+#include "fft_common.h"
+#include "mkid_internal.h"
+
+namespace mkid {
+
+template <int N>
+struct FGeo {
+    static constexpr int PTS = 8, NT = N / PTS, FPB = 4;
+    static constexpr int BT = NT * FPB;                 // == C: one channel per thread
+    static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
+    static constexpr int RS = 2 * T - 1 + FPB;          // ring slots (hops)
+    static constexpr int LDSF = lds_frame_elems<N>();
+    static constexpr int SPT = FPB * M / BT;            // new samples per thread per iteration
+    static_assert(SPT == 4, "one 16-byte load per thread per iteration");
+    static_assert(BT == C, "one channel per thread");
+    static constexpr int NS2 = Plan8<N>::R[0], NS3 = NS2 * Plan8<N>::R[1], NS4 = NS3 * Plan8<N>::R[2];
+    static constexpr size_t lds_bytes = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8 + (size_t)N * 16;
+    static constexpr int HIST = (2 * T - 1 + kLpfHist) * M;  // ADC history samples
+    // register budget sized for 4 waves per SIMD (16 per CU, <= 128 VGPRs): HIP's second
+    // launch-bounds argument is the minimum waves per execution unit
+    static constexpr int MINW = 4;
+};
+
+// The 16 bytes (4 samples) this thread contributes to the FPB hops starting at first_hop.
+template <int N>
+__device__ __forceinline__ uint4 front_load(const FrontArgs& a, int64_t first_hop, int tid) {
+    using G = FGeo<N>;
+    const int64_t s0 = first_hop * G::M + (int64_t)tid * G::SPT;  // sample index in chunk
+    if (s0 >= a.K * G::M) return make_uint4(0, 0, 0, 0);
+    if (s0 >= -a.avail) return *reinterpret_cast<const uint4*>(a.x + s0);
+    return *reinterpret_cast<const uint4*>(a.xhist + (s0 + a.avail + G::HIST));
+}
+
+template <int N>
+__global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs a) {
+    using G = FGeo<N>;
+    using PL = Plan8<N>;
+    constexpr int PTS = G::PTS, NT = G::NT, M = G::M, C = G::C, T = G::T, RS = G::RS, FPB = G::FPB;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
+    float2* fbuf = reinterpret_cast<float2*>(smem + (size_t)RS * M * 4);
+
+    const int tid = threadIdx.x;
+    const int slot = tid / NT;  // frame of the iteration this thread transforms
+    const int t = tid % NT;
+    float2* buf = fbuf + slot * G::LDSF;
+    // PFB taps of point p as one float4 {h[p], h[N+p], h[2N+p], h[3N+p]} in LDS (registers are
+    // the scarce resource at 1024 threads: the low-pass accumulators live there)
+    float4* hl = reinterpret_cast<float4*>(smem + (size_t)RS * M * 4 + (size_t)FPB * G::LDSF * 8);
+    static_assert(T == 4, "one float4 of taps per point");
+    for (int p = tid; p < N; p += G::BT)
+        hl[p] = make_float4(a.pfb[p], a.pfb[N + p], a.pfb[2 * N + p], a.pfb[3 * N + p]);
+
+    TwiddleRec<N, PTS, PL::R[1], G::NS2> tw2;
+    tw2.init(t);
+    TwiddleRec<N, PTS, PL::R[2], G::NS3> tw3;
+    tw3.init(t);
+    TwiddleRec<N, PTS, (PL::NP == 4 ? PL::R[3] : 2), G::NS4> tw4;
+    if constexpr (PL::NP == 4) tw4.init(t);
+
+    const int c = tid;  // channel of the select / low-pass / phase stage
+    const int32_t bin = a.bins[c];
+    const float ic = a.ic[c], qc = a.qc[c];
+    const int podd_mask = bin & 1;
+
+    const int64_t k_b = (int64_t)blockIdx.x * a.frames_per_block;
+    int64_t k_e = k_b + a.frames_per_block;
+    if (k_e > a.K) k_e = a.K;
+    if (k_b >= k_e) return;
+    const int64_t k_start = k_b - kLpfHist;  // warm-up frames rebuild the low-pass history
+
+    // prologue: hops k_start-2T+1 .. k_start+FPB-1 -> ring (slot = hop mod RS)
+    {
+        const int64_t h0 = k_start - 2 * T + 1;
+        for (int g = 0; g < RS; g += FPB) {
+            const int64_t hop = h0 + g + (tid * G::SPT) / M;
+            if (hop > h0 + RS - 1) continue;
+            const uint4 v = front_load<N>(a, h0 + g, tid);
+            *reinterpret_cast<uint4*>(ring + (int)(((hop % RS) + RS) % RS) * M + (tid * G::SPT) % M) = v;
+        }
+    }
+    uint4 pre = front_load<N>(a, k_start + FPB, tid);
+    __syncthreads();
+
+    float2 acc[13];
+#pragma unroll
+    for (int m = 0; m < 13; ++m) acc[m] = make_float2(0.f, 0.f);
+    float2 ys = make_float2(0.f, 0.f);
+
+    for (int64_t kb = k_start; kb < k_e; kb += FPB) {
+        // LO rows of this iteration's frames (latency hidden behind the FFT)
+        float2 lov[FPB];
+#pragma unroll
+        for (int f = 0; f < FPB; ++f) lov[f] = a.lo[(int64_t)((a.k0 + kb + f) & (a.P - 1)) * C + c];
+
+        // ---- PFB of frame kb + slot from the LDS ring ----
+        const int64_t h_first = kb + slot + 1 - 2 * T;
+        const int sb = (int)(((h_first % RS) + RS) % RS);
+        float2 v[PTS];
+#pragma unroll
+        for (int r = 0; r < PTS; ++r) {
+            const int p = t + r * NT;
+            const int hi = p / M, off = p % M;
+            const float4 h4 = hl[p];
+            const float hh[T] = {h4.x, h4.y, h4.z, h4.w};
+            float ur = 0.f, ui = 0.f;
+#pragma unroll
+            for (int tau = 0; tau < T; ++tau) {
+                int sl = sb + 2 * tau + hi;
+                sl -= sl >= RS ? RS : 0;  // sb + 2 tau + hi < 2 RS
+                const uint32_t w = ring[sl * M + off];
+                ur = fmaf(hh[tau], (float)(int16_t)(w & 0xffffu), ur);
+                ui = fmaf(hh[tau], (float)(int16_t)(w >> 16), ui);
+            }
+            v[r] = make_float2(ur, ui);
+            // keep the point order: stops the scheduler from hoisting all 32 ring loads at once
+            asm volatile("" : "+v"(v[r].x), "+v"(v[r].y));
+        }
+        st_dft<PTS, PL::R[0]>(v);
+        __syncthreads();  // ring reads of this iteration and last iteration's select are done
+        {
+            const int64_t hop = kb + FPB + (tid * G::SPT) / M;
+            *reinterpret_cast<uint4*>(ring + (int)(((hop % RS) + RS) % RS) * M + (tid * G::SPT) % M) = pre;
+            pre = front_load<N>(a, kb + 2 * FPB, tid);
+        }
+        st_write<N, PTS, PL::R[0], 1>(buf, v, t);
+        __syncthreads();
+        st_read<N, PTS, PL::R[1]>(buf, v, t);
+        __syncthreads();
+        tw2.apply(v);
+        st_dft<PTS, PL::R[1]>(v);
+        st_write<N, PTS, PL::R[1], G::NS2>(buf, v, t);
+        __syncthreads();
+        st_read<N, PTS, PL::R[2]>(buf, v, t);
+        __syncthreads();
+        tw3.apply(v);
+        st_dft<PTS, PL::R[2]>(v);
+        st_write<N, PTS, PL::R[2], G::NS3>(buf, v, t);
+        __syncthreads();
+        if constexpr (PL::NP == 4) {
+            st_read<N, PTS, PL::R[3]>(buf, v, t);
+            __syncthreads();
+            tw4.apply(v);
+            st_dft<PTS, PL::R[3]>(v);
+            st_write<N, PTS, PL::R[3], G::NS4>(buf, v, t);
+            __syncthreads();
+        }
+
+        // ---- select + DDC + low-pass + phase for channel c over the FPB frames ----
+#pragma unroll
+        for (int f = 0; f < FPB; ++f) {
+            const int64_t k = kb + f;
+            float2 X = fbuf[f * G::LDSF + lpad(bin)];
+            if ((int)((a.k0 + k + 1) & 1) & podd_mask) X = make_float2(-X.x, -X.y);
+            const float2 z = cmul(X, lov[f]);
+            if ((f & 1) == 0) {  // frame 2j: taps 1,3,..,25 into outputs j..j+12
+#pragma unroll
+                for (int m = 0; m < 13; ++m) {
+                    acc[m].x = fmaf(a.taps.g[2 * m + 1], z.x, acc[m].x);
+                    acc[m].y = fmaf(a.taps.g[2 * m + 1], z.y, acc[m].y);
+                }
+            } else {  // frame 2j+1: taps 0,2,..,24; output j complete
+#pragma unroll
+                for (int m = 0; m < 13; ++m) {
+                    acc[m].x = fmaf(a.taps.g[2 * m], z.x, acc[m].x);
+                    acc[m].y = fmaf(a.taps.g[2 * m], z.y, acc[m].y);
+                }
+                const float2 y = acc[0];
+#pragma unroll
+                for (int m = 0; m < 12; ++m) acc[m] = acc[m + 1];
+                acc[12] = make_float2(0.f, 0.f);
+                if (k > k_b && k < k_e) {
+                    const int64_t j = (k - 1) >> 1;
+                    ys.x += y.x;
+                    ys.y += y.y;
+                    const float ph = atan2f(y.y - qc, y.x - ic);
+                    int q = __float2int_rn(ph * 8192.0f);
+                    q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
+                    if (a.phase) a.phase[j * C + c] = ph;
+                    a.raw[j * C + c] = (int16_t)q;
+                }
+            }
+        }
+    }
+    if (a.ysum) {
+        atomicAdd(&a.ysum[c].x, ys.x);
+        atomicAdd(&a.ysum[c].y, ys.y);
+    }
+}
+
+bool front_supported(int N) { return N == 128 || N == 256 || N == 512 || N == 1024 || N == 2048; }
+
+int64_t front_hist_samples(int N) { return (int64_t)(2 * kPfbTaps - 1 + kLpfHist) * (N / 2); }
+
+template <int N>
+static hipError_t launch_front_n(const FrontArgs& a0, hipStream_t s) {
+    using G = FGeo<N>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_front<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)G::lds_bytes);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    FrontArgs a = a0;
+    if (a.K <= 0) return hipSuccess;
+    // frame runs: long enough to amortise the 24-frame warm-up, enough of them to fill the CUs
+    int64_t fpb = a.K / 1024;
+    fpb = fpb < 64 ? 64 : (fpb > 1024 ? 1024 : fpb);
+    fpb = (fpb + G::FPB - 1) / G::FPB * G::FPB;
+    a.frames_per_block = fpb;
+    const int64_t blocks = (a.K + fpb - 1) / fpb;
+    hipLaunchKernelGGL(k_front<N>, dim3((unsigned)blocks), dim3(G::BT), G::lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_front(int N, const FrontArgs& a, hipStream_t s) {
+    switch (N) {
+        case 128: return launch_front_n<128>(a, s);
+        case 256: return launch_front_n<256>(a, s);
+        case 512: return launch_front_n<512>(a, s);
+        case 1024: return launch_front_n<1024>(a, s);
+        case 2048: return launch_front_n<2048>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mkid

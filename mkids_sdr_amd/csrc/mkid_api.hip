@@ -60,8 +60,17 @@ struct mkid_ctx {
     int16_t *d_rhist = nullptr, *d_rtmp = nullptr;
     TrigState* d_tstate = nullptr;
     int64_t k0 = 0, j0 = 0;
+    // two-stream pipeline: stream A (= `stream`) runs the channeliser, stream B the low-pass,
+    // trigger and compaction of the previous sub-chunk; z is double-buffered between them.
+    hipStream_t sB = nullptr;
+    hipEvent_t ev_zready[2] = {nullptr, nullptr}, ev_zfree[2] = {nullptr, nullptr};
+    hipEvent_t ev_start = nullptr, ev_done = nullptr;
+    int zi = 0;
+    int64_t G = 0;  // pipeline sub-chunk (samples)
+    bool fused = false;  // K1-K6 in k_front (no z buffers, no stream B work)
+    int64_t H = 0;       // ADC history samples carried between calls
     // workspace
-    float2* d_z = nullptr;
+    float2* d_zb[2] = {nullptr, nullptr};
     int16_t* d_raw = nullptr;
     float2* d_ysum = nullptr;
     uint64_t* d_slots = nullptr;     // [C][nseg][capseg]
@@ -72,7 +81,8 @@ struct mkid_ctx {
     int32_t* d_reruns = nullptr;     // [C]
     int64_t nseg_max = 0, slot_cap = 0, scratch_cap = 0;
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
-    int64_t last_J = 0;
+    int64_t last_J = 0;     // phase rows of the last call
+    int64_t last_subJ = 0;  // rows of its last sub-chunk (held in d_raw)
     // host-API staging (lazy)
     uint32_t* d_in = nullptr;
     float* d_phase_ws = nullptr;
@@ -111,19 +121,19 @@ static hipEvent_t get_event(mkid_ctx* c) {
     return e;
 }
 
-static void tstart(mkid_ctx* c, int k, KTime* kt) {
+static void tstart(mkid_ctx* c, int k, KTime* kt, hipStream_t s) {
     kt->k = -1;
     if (!c->timing) return;
     kt->a = get_event(c);
     kt->b = get_event(c);
     if (!kt->a || !kt->b) return;
     kt->k = k;
-    (void)hipEventRecord(kt->a, c->stream);
+    (void)hipEventRecord(kt->a, s);
 }
 
-static void tstop(mkid_ctx* c, KTime* kt) {
+static void tstop(mkid_ctx* c, KTime* kt, hipStream_t s) {
     if (kt->k < 0) return;
-    (void)hipEventRecord(kt->b, c->stream);
+    (void)hipEventRecord(kt->b, s);
     c->pending.push_back(*kt);
 }
 
@@ -144,7 +154,7 @@ static int flush_timing(mkid_ctx* c) {
 static void free_all(mkid_ctx* c) {
     void* ptrs[] = {c->d_pfb,   c->d_bins,  c->d_lo,    c->d_fir,    c->d_ic,     c->d_qc,
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
-                    c->d_rtmp,  c->d_tstate, c->d_z,    c->d_raw,    c->d_ysum,   c->d_slots,
+                    c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
                     c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns};
     for (void* p : ptrs)
@@ -154,6 +164,10 @@ static void free_all(mkid_ctx* c) {
         (void)hipEventDestroy(kt.b);
     }
     for (auto e : c->pool) (void)hipEventDestroy(e);
+    hipEvent_t evs[] = {c->ev_zready[0], c->ev_zready[1], c->ev_zfree[0], c->ev_zfree[1], c->ev_start, c->ev_done};
+    for (auto e : evs)
+        if (e) (void)hipEventDestroy(e);
+    if (c->sB) (void)hipStreamDestroy(c->sB);
     if (c->own) (void)hipStreamDestroy(c->own);
 }
 
@@ -205,6 +219,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     if (P <= 0 || (P & (P - 1)) != 0) { g_err = "dds_entries must be a power of two"; return MKID_E_ARG; }
     if (cfg->max_chunk < N || cfg->max_chunk % N != 0) { g_err = "max_chunk must be a positive multiple of N"; return MKID_E_ARG; }
     if (cfg->dead_time < 0) { g_err = "dead_time < 0"; return MKID_E_ARG; }
+    if (cfg->front != MKID_FRONT_AUTO && cfg->front != MKID_FRONT_SPLIT) { g_err = "bad front mode"; return MKID_E_ARG; }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { g_err = "no HIP device"; return MKID_E_NODEV; }
     if (device < 0 || device >= ndev) { g_err = "bad device index"; return MKID_E_ARG; }
@@ -213,8 +228,17 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->cfg = *cfg;
     c->device = device;
     c->C = C; c->N = N; c->M = N / 2; c->T = kPfbTaps; c->P = P;
-    c->Kmax = cfg->max_chunk / c->M;
-    c->Jmax = cfg->max_chunk / N;
+    c->fused = cfg->front == MKID_FRONT_AUTO && front_supported(N);
+    // split front end: a large call is cut into 4 sub-chunks so the channeliser (stream A) of
+    // sub-chunk i+1 overlaps the low-pass/trigger (stream B) of sub-chunk i
+    int64_t G = cfg->max_chunk;
+    if (!c->fused && G >= (int64_t)512 * N) {
+        G = cfg->max_chunk / 4;
+        G -= G % N;
+    }
+    c->G = G;
+    c->Kmax = G / c->M;
+    c->Jmax = G / N;
     // Packet capacities are hard bounds: an event needs >= dead_time + 3 phase samples (trigger,
     // peak, dead time, re-arm), so no per-channel/segment overflow can occur.
     const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // whole call, one segment
@@ -223,7 +247,8 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     const int64_t capseg = seg_capacity(cfg->dead_time);
     c->slot_cap = std::max<int64_t>((int64_t)C * c->nseg_max * capseg, (int64_t)C * c->capc);
     c->scratch_cap = std::max<int64_t>(capseg, c->capc);
-    const int H = c->T * N - c->M;
+    c->H = c->fused ? front_hist_samples(N) : (int64_t)c->T * N - c->M;
+    const int64_t H = c->H;
     auto fail = [&](hipError_t e, const char* what) {
         g_err = std::string(what) + ": " + hipGetErrorString(e);
         free_all(c);
@@ -235,6 +260,11 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     if ((e = hipSetDevice(device)) != hipSuccess) return fail(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess) return fail(e, "hipStreamCreate");
     c->stream = c->own;
+    if ((e = hipStreamCreateWithFlags(&c->sB, hipStreamNonBlocking)) != hipSuccess) return fail(e, "hipStreamCreate B");
+    for (hipEvent_t* ev : {&c->ev_zready[0], &c->ev_zready[1], &c->ev_zfree[0], &c->ev_zfree[1], &c->ev_start, &c->ev_done})
+        if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return fail(e, "hipEventCreate");
+    for (int b = 0; b < 2; ++b)
+        if ((e = hipEventRecord(c->ev_zfree[b], c->sB)) != hipSuccess) return fail(e, "hipEventRecord");
     AL(d_pfb, (size_t)c->T * N);
     AL(d_bins, C);
     AL(d_lo, (size_t)C * P);
@@ -249,7 +279,10 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_rhist, (size_t)kRawHist * C);
     AL(d_rtmp, (size_t)kRawHist * C);
     AL(d_tstate, C);
-    AL(d_z, (size_t)c->Kmax * C);
+    if (!c->fused) {
+        AL(d_zb[0], (size_t)c->Kmax * C);
+        AL(d_zb[1], (size_t)c->Kmax * C);
+    }
     AL(d_raw, (size_t)c->Jmax * C);
     AL(d_ysum, C);
     AL(d_slots, (size_t)c->slot_cap);
@@ -337,8 +370,13 @@ int mkid_set_bins(mkid_ctx* c, const int32_t* bins, int32_t n) {
 int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
     if (!c || !li || !lq) return MKID_E_ARG;
     if (P != c->P) FAIL(c, MKID_E_ARG, "entries_per_ch must equal cfg.dds_entries");
+    // device layout [P][C] (input is [C][P]): one frame reads one contiguous row
     std::vector<float2> lo((size_t)c->C * P);
-    for (size_t i = 0; i < lo.size(); ++i) lo[i] = make_float2(li[i] / 32768.f, -lq[i] / 32768.f);
+    for (int ch = 0; ch < c->C; ++ch)
+        for (int p = 0; p < P; ++p) {
+            const size_t i = (size_t)ch * P + p;
+            lo[(size_t)p * c->C + ch] = make_float2(li[i] / 32768.f, -lq[i] / 32768.f);
+        }
     return upload(c, c->d_lo, lo.data(), lo.size() * 8);
 }
 
@@ -383,8 +421,8 @@ int mkid_set_baseline(mkid_ctx* c, int32_t mode, int32_t alpha, int32_t kf, int3
 int mkid_reset_stream(mkid_ctx* c) {
     if (!c) return MKID_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    const int H = c->T * c->N - c->M;
-    HIPCHK(c, hipMemsetAsync(c->d_xhist, 0, (size_t)H * 4, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->sB));
+    HIPCHK(c, hipMemsetAsync(c->d_xhist, 0, (size_t)c->H * 4, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_zhist, 0, (size_t)kLpfHist * c->C * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_rhist, 0, (size_t)kRawHist * c->C * 2, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_tstate, 0, (size_t)c->C * sizeof(TrigState), c->stream));
@@ -393,6 +431,81 @@ int mkid_reset_stream(mkid_ctx* c) {
     c->k0 = 0;
     c->j0 = 0;
     c->last_J = 0;
+    c->last_subJ = 0;
+    return MKID_OK;
+}
+
+// K7 + K8 on stream s for the J phase rows in d_raw: matched filter, baseline, trigger state
+// machine (speculative segments + fix-up), raw-phase history roll, packet compaction.
+static int run_trigger(mkid_ctx* c, int64_t J, uint64_t* d_events, int64_t cap, int64_t* d_counts,
+                       hipStream_t s) {
+    const int C = c->C;
+    KTime kt;
+    const bool serial = c->mode == MKID_BASE_SVF || J <= kSegL;
+    const int32_t L = serial ? (int32_t)J : (int32_t)kSegL;
+    const int32_t W = serial ? 0 : (int32_t)kSegW;
+    const int32_t nseg = serial ? 1 : (int32_t)((J + kSegL - 1) / kSegL);
+    const int32_t capseg = serial ? (int32_t)(J / (c->cfg.dead_time + 3) + 2) : (int32_t)seg_capacity(c->cfg.dead_time);
+    TrigSpecArgs ta{c->d_raw,   c->d_rhist, c->d_fir,  c->d_thr,     c->d_tstate,  c->d_tstate,
+                    c->d_sspec, c->d_send,  c->d_slots, c->d_chcounts, c->d_scratch, c->d_reruns,
+                    J,          c->j0,      C,          nseg,          L,            W,
+                    capseg,     c->mode,    c->alpha,   c->kf,         c->kq,        c->base_thr,
+                    c->cfg.dead_time};
+    tstart(c, MKID_K_TRIGGER, &kt, s);
+    HIPCHK(c, launch_trigger(ta, s));
+    tstop(c, &kt, s);
+    HIPCHK(c, launch_hist_roll(c->d_rtmp, c->d_rhist, c->d_raw, kRawHist, J, (int64_t)C * 2, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_rhist, c->d_rtmp, (size_t)kRawHist * C * 2, hipMemcpyDeviceToDevice, s));
+
+    tstart(c, MKID_K_COMPACT, &kt, s);
+    HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, (int64_t)C * nseg, capseg, d_events, cap, d_counts,
+                             c->d_scan, s));
+    tstop(c, &kt, s);
+    return MKID_OK;
+}
+
+// Fused front end: one k_front launch per chunk (ADC -> phase, raw), then K7/K8, all on the
+// context stream; chunks of max_chunk samples.
+static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
+                         int64_t cap, int64_t* d_counts) {
+    const int C = c->C, N = c->N, M = c->M;
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 8, s));
+    const uint32_t* x = (const uint32_t*)d_iq;
+    c->last_J = 0;
+    for (int64_t off = 0; off < n; off += c->G) {
+        const int64_t S = std::min<int64_t>(c->G, n - off);
+        const int64_t K = S / M, J = S / N;
+        KTime kt;
+        FrontArgs fa{};
+        fa.x = x + off;
+        fa.xhist = c->d_xhist;
+        fa.pfb = c->d_pfb;
+        fa.bins = c->d_bins;
+        fa.lo = c->d_lo;
+        fa.ic = c->d_ic;
+        fa.qc = c->d_qc;
+        fa.phase = d_phase ? d_phase + (off / N) * C : nullptr;
+        fa.raw = c->d_raw;
+        fa.ysum = c->d_ysum;
+        fa.K = K;
+        fa.k0 = c->k0;
+        fa.avail = off;
+        fa.P = c->P;
+        fa.taps = c->lpf;
+        tstart(c, MKID_K_FRONT, &kt, s);
+        HIPCHK(c, launch_front(N, fa, s));
+        tstop(c, &kt, s);
+        int r = run_trigger(c, J, d_events, cap, d_counts, s);
+        if (r) return r;
+        c->k0 += K;
+        c->j0 += J;
+        c->last_J += J;
+        c->last_subJ = J;
+    }
+    HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, c->H, n, 4, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)c->H * 4, hipMemcpyDeviceToDevice, s));
     return MKID_OK;
 }
 
@@ -402,55 +515,68 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
     if (((uintptr_t)d_iq & 15) != 0) FAIL(c, MKID_E_ARG, "d_iq must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->fused) return process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts);
     const int C = c->C, N = c->N, M = c->M;
-    const int H = c->T * N - M;
-    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 8, c->stream));
+    const int64_t H = c->H;
+    hipStream_t A = c->stream, B = c->sB;
+    // B joins A's order (inputs written by earlier work on A, previous calls) ...
+    HIPCHK(c, hipEventRecord(c->ev_start, A));
+    HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
+    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, B));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 8, B));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
-    for (int64_t off = 0; off < n; off += c->cfg.max_chunk) {
-        const int64_t S = std::min<int64_t>(c->cfg.max_chunk, n - off);
+    const float2* zprev = c->d_zhist;  // the 24 frames before the current sub-chunk
+    for (int64_t off = 0; off < n; off += c->G) {
+        const int64_t S = std::min<int64_t>(c->G, n - off);
         const int64_t K = S / M, J = S / N;
+        const int b = c->zi;
+        float2* z = c->d_zb[b];
         KTime kt;
-        ChanArgs ca{x + off, c->d_xhist, c->d_pfb, c->d_bins, c->d_lo, c->d_z, K, c->k0, c->P, 0, 0};
-        tstart(c, MKID_K_CHANNELIZE, &kt);
-        HIPCHK(c, launch_channelize(N, ca, c->stream));
-        tstop(c, &kt);
-        HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x + off, H, S, 4, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)H * 4, hipMemcpyDeviceToDevice, c->stream));
+        // ---- stream A: channeliser into z[b] once its last reader is done ----
+        HIPCHK(c, hipStreamWaitEvent(A, c->ev_zfree[b], 0));
+        ChanArgs ca{x + off, c->d_xhist, c->d_pfb, c->d_bins, c->d_lo, z, K, c->k0, c->P, 0, 0, off};
+        tstart(c, MKID_K_CHANNELIZE, &kt, A);
+        HIPCHK(c, launch_channelize(N, ca, A));
+        tstop(c, &kt, A);
+        HIPCHK(c, hipEventRecord(c->ev_zready[b], A));
 
-        LpfArgs la{c->d_z, c->d_zhist, c->d_ic, c->d_qc, d_phase ? d_phase + (off / N) * C : nullptr,
+        // ---- stream B: low-pass + phase, trigger, compaction of this sub-chunk ----
+        HIPCHK(c, hipStreamWaitEvent(B, c->ev_zready[b], 0));
+        LpfArgs la{z, zprev, c->d_ic, c->d_qc, d_phase ? d_phase + (off / N) * C : nullptr,
                    c->d_raw, c->d_ysum, J, C, c->lpf};
-        tstart(c, MKID_K_FIR_PHASE, &kt);
-        HIPCHK(c, launch_lpf_phase(la, c->stream));
-        tstop(c, &kt);
-        HIPCHK(c, launch_hist_roll(c->d_ztmp, c->d_zhist, c->d_z, kLpfHist, K, (int64_t)C * 8, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->d_zhist, c->d_ztmp, (size_t)kLpfHist * C * 8, hipMemcpyDeviceToDevice, c->stream));
+        tstart(c, MKID_K_FIR_PHASE, &kt, B);
+        HIPCHK(c, launch_lpf_phase(la, B));
+        tstop(c, &kt, B);
+        if (off + S >= n || K < kLpfHist) {
+            // carry the trailing 24 frames through d_zhist: always at the end of a call (next
+            // call's history), and between sub-chunks too short to hold them
+            HIPCHK(c, launch_hist_roll(c->d_ztmp, zprev, z, kLpfHist, K, (int64_t)C * 8, B));
+            HIPCHK(c, hipMemcpyAsync(c->d_zhist, c->d_ztmp, (size_t)kLpfHist * C * 8, hipMemcpyDeviceToDevice, B));
+            zprev = c->d_zhist;
+            HIPCHK(c, hipEventRecord(c->ev_zfree[b], B));
+        } else {
+            zprev = z + (K - kLpfHist) * C;  // read in place by the next sub-chunk's low-pass
+        }
+        // the previous sub-chunk's buffer (history of the low-pass above) may now be overwritten
+        HIPCHK(c, hipEventRecord(c->ev_zfree[b ^ 1], B));
+        c->zi ^= 1;
 
-        const bool serial = c->mode == MKID_BASE_SVF || J <= kSegL;
-        const int32_t L = serial ? (int32_t)J : (int32_t)kSegL;
-        const int32_t W = serial ? 0 : (int32_t)kSegW;
-        const int32_t nseg = serial ? 1 : (int32_t)((J + kSegL - 1) / kSegL);
-        const int32_t capseg = serial ? (int32_t)(J / (c->cfg.dead_time + 3) + 2) : (int32_t)seg_capacity(c->cfg.dead_time);
-        TrigSpecArgs ta{c->d_raw,    c->d_rhist,   c->d_fir,    c->d_thr,    c->d_tstate, c->d_tstate,
-                        c->d_sspec,  c->d_send,    c->d_slots,  c->d_chcounts, c->d_scratch, c->d_reruns,
-                        J,           c->j0,        C,           nseg,        L,           W,
-                        capseg,      c->mode,      c->alpha,    c->kf,       c->kq,       c->base_thr,
-                        c->cfg.dead_time};
-        tstart(c, MKID_K_TRIGGER, &kt);
-        HIPCHK(c, launch_trigger(ta, c->stream));
-        tstop(c, &kt);
-        HIPCHK(c, launch_hist_roll(c->d_rtmp, c->d_rhist, c->d_raw, kRawHist, J, (int64_t)C * 2, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->d_rhist, c->d_rtmp, (size_t)kRawHist * C * 2, hipMemcpyDeviceToDevice, c->stream));
-
-        tstart(c, MKID_K_COMPACT, &kt);
-        HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, (int64_t)C * nseg, capseg, d_events, cap, d_counts,
-                                 c->d_scan, c->stream));
-        tstop(c, &kt);
+        {
+            int r = run_trigger(c, J, d_events, cap, d_counts, B);
+            if (r) return r;
+        }
         c->k0 += K;
         c->j0 += J;
         c->last_J += J;
+        c->last_subJ = J;
     }
+    // ADC history for the next call (all readers of d_xhist are channeliser launches on A)
+    HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, H, n, 4, A));
+    HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)H * 4, hipMemcpyDeviceToDevice, A));
+    // ... and A (the caller's stream) waits for everything B did
+    HIPCHK(c, hipEventRecord(c->ev_done, B));
+    HIPCHK(c, hipStreamWaitEvent(A, c->ev_done, 0));
     return MKID_OK;
 }
 
@@ -460,10 +586,11 @@ int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, ui
     if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t chunk = c->cfg.max_chunk;
-    const int64_t evcap = (int64_t)c->C * c->capc;
+    // hard bound for a whole call of `chunk` samples (per channel: J/(dead+3)+2 packets)
+    const int64_t evcap = (int64_t)c->C * ((chunk / c->N) / (c->cfg.dead_time + 3) + 2);
     if (!c->d_in) {
         HIPCHK(c, dalloc(&c->d_in, (size_t)chunk));
-        HIPCHK(c, dalloc(&c->d_phase_ws, (size_t)c->Jmax * c->C));
+        HIPCHK(c, dalloc(&c->d_phase_ws, (size_t)(chunk / c->N) * c->C));
         HIPCHK(c, dalloc(&c->d_ev_ws, (size_t)evcap));
     }
     int64_t produced = 0, written = 0;
@@ -497,7 +624,7 @@ int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, ui
 int mkid_last_raw_phase(mkid_ctx* c, const int16_t** d_raw, int64_t* nrows) {
     if (!c || !d_raw || !nrows) return MKID_E_ARG;
     *d_raw = c->d_raw;
-    *nrows = std::min(c->last_J, c->Jmax);
+    *nrows = std::min(c->last_subJ, c->Jmax);
     return MKID_OK;
 }
 
@@ -546,7 +673,7 @@ int mkid_get_timing(mkid_ctx* c, int32_t k, double* total_ms, int64_t* launches)
 }
 
 const char* mkid_kernel_name(int32_t k) {
-    static const char* names[MKID_K_COUNT] = {"k_channelize", "k_lpf_phase", "k_trigger", "k_compact"};
+    static const char* names[MKID_K_COUNT] = {"k_channelize", "k_lpf_phase", "k_trigger", "k_compact", "k_front"};
     return (k >= 0 && k < MKID_K_COUNT) ? names[k] : "?";
 }
 

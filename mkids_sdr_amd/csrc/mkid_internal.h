@@ -29,13 +29,15 @@ struct ChanArgs {
     const uint32_t* xhist;  // T*N - M previous samples
     const float* pfb;       // T*N prototype
     const int32_t* bins;    // C
-    const float2* lo;       // C*P, conj(LUT)/2^15
+    const float2* lo;       // [P][C], conj(LUT)/2^15
     float2* z;              // [K][C]
     int64_t K;              // frames in this chunk
     int64_t k0;             // global index of the chunk's first frame
     int32_t P;              // LO period (power of two)
     int32_t pad;
     int64_t frames_per_block;  // set by the launcher
+    int64_t avail;          // samples readable before x (earlier sub-chunks of the same call);
+                            // older samples come from xhist
 };
 
 struct LpfArgs {
@@ -48,6 +50,26 @@ struct LpfArgs {
     float2* ysum;           // [C] per-channel sum of y (avgIQ) or nullptr
     int64_t J;
     int32_t C;
+    LpfTaps taps;
+};
+
+struct FrontArgs {
+    const uint32_t* x;      // chunk, int16 I/Q packed per 32-bit word
+    const uint32_t* xhist;  // front_hist_samples(N) previous samples
+    const float* pfb;       // T*N prototype
+    const int32_t* bins;    // C
+    const float2* lo;       // [P][C], conj(LUT)/2^15
+    const float* ic;        // C
+    const float* qc;        // C
+    float* phase;           // [K/2][C] or nullptr
+    int16_t* raw;           // [K/2][C]
+    float2* ysum;           // [C] or nullptr
+    int64_t K;              // frames in this chunk (even)
+    int64_t k0;             // global index of the chunk's first frame
+    int64_t frames_per_block;  // set by the launcher
+    int64_t avail;          // samples readable before x (earlier sub-chunks of the same call)
+    int32_t P;              // LO period (power of two)
+    int32_t pad;
     LpfTaps taps;
 };
 
@@ -73,6 +95,7 @@ struct TrigSpecArgs {
 // launchers (return hipError_t of the launch)
 hipError_t launch_channelize(int N, const ChanArgs& a, hipStream_t s);
 hipError_t launch_lpf_phase(const LpfArgs& a, hipStream_t s);
+hipError_t launch_front(int N, const FrontArgs& a, hipStream_t s);
 hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s);
 hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
                           int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
@@ -85,5 +108,7 @@ hipError_t launch_synth(int16_t* out, int64_t n, int64_t n0, const int16_t* base
                         hipStream_t s);
 
 bool channelize_supported(int N);
+bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length
+int64_t front_hist_samples(int N);  // ADC history the fused kernel reads before a chunk
 
 }  // namespace mkid

@@ -46,10 +46,10 @@ def split_by_channel(ev):
     return out
 
 
-def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32):
+def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32, front='auto'):
     from mkids_sdr_amd.channelizer import Channelizer
     S = case.iq.shape[0]
-    ch = Channelizer(case.C, max_chunk=max_chunk or S, dead_time=dead)
+    ch = Channelizer(case.C, max_chunk=max_chunk or S, dead_time=dead, front=front)
     try:
         configure(ch, case, thr, mode)
         phases, evs = [], []
@@ -63,12 +63,12 @@ def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32):
     return np.concatenate(phases), np.concatenate(evs), (mi, mq)
 
 
-def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=True):
+def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=True, front='auto'):
     o = signals.oracle_chain(case)
     r = o.process(case.iq)
     tr = otrig.Trigger(case.C, case.fir12, thr, mode=mode, dead=dead)
     ev_o, n_o, _ = tr.run(r['raw'])
-    ph_g, ev_g, _ = run_gpu(case, thr, splits, mode, max_chunk, dead)
+    ph_g, ev_g, _ = run_gpu(case, thr, splits, mode, max_chunk, dead, front)
 
     assert ph_g.shape == r['phase'].shape
     tones = slice(0, case.n_tones)
@@ -107,18 +107,22 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     return ph_g, ev_g, r
 
 
-@pytest.mark.parametrize('C,S,splits,seed', [
-    (64, 2 ** 16, None, 1),                       # config 1 geometry (64 ch, 2^16 samples)
-    (128, 2 ** 17, [0, 2 ** 15, 2 ** 17], 2),
-    (256, 2 ** 18, [0, 2 ** 16 + 512, 2 ** 17, 2 ** 18], 3),   # config 2 geometry, streamed
-    (512, 2 ** 18, None, 4),
-    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5),    # config 3 geometry
-    (2048, 2 ** 20, None, 6),                     # config 5 geometry
+@pytest.mark.parametrize('C,S,splits,seed,front', [
+    (64, 2 ** 16, None, 1, 'auto'),                 # config 1 geometry (64 ch, 2^16 samples)
+    (128, 2 ** 17, [0, 2 ** 15, 2 ** 17], 2, 'auto'),
+    (256, 2 ** 18, [0, 2 ** 16 + 512, 2 ** 17, 2 ** 18], 3, 'auto'),   # config 2, streamed
+    (256, 2 ** 18, [0, 2 ** 16 + 512, 2 ** 17, 2 ** 18], 3, 'split'),
+    (512, 2 ** 18, None, 4, 'auto'),
+    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'auto'),    # config 3 geometry
+    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'split'),
+    (2048, 2 ** 20, None, 6, 'auto'),               # config 5 geometry (split front: N = 4096)
 ])
-def test_chain_parity(gpu, C, S, splits, seed):
+def test_chain_parity(gpu, C, S, splits, seed, front):
+    """Full chain vs the oracle. 'auto' runs the fused k_front kernel for N <= 2048; 'split'
+    runs k_channelize + k_lpf_phase with z staged in HBM."""
     case = signals.make_case(C, S, seed=seed, pulses_per_ch=max(1.0, S / (2 * C) / 400))
     thr = quiet_thresholds(C, min(S, 2 * C * 2048), seed)
-    compare(case, thr, splits or [0, S])
+    compare(case, thr, splits or [0, S], front=front)
 
 
 @pytest.mark.parametrize('mode', [0, 1, 2])
@@ -139,8 +143,26 @@ def test_internal_subchunks_and_tiny_calls(gpu):
     case = signals.make_case(C, S, seed=21, pulses_per_ch=2.0)
     thr = quiet_thresholds(C, S, 21)
     compare(case, thr, [0, S], max_chunk=8 * 2 * C)
+    compare(case, thr, [0, S], max_chunk=8 * 2 * C, front='split')
     splits = list(range(0, 40 * 2 * C, 2 * C)) + [S]
     compare(case, thr, splits)
+    compare(case, thr, splits, front='split')
+
+
+def test_pipelined_subchunks(gpu):
+    """max_chunk >= 512 N: calls are split into max_chunk/4 sub-chunks whose channeliser runs on
+    a second stream ahead of the low-pass/trigger (double-buffered z). Ragged calls leave short
+    last sub-chunks (down to one FFT frame pair)."""
+    C = 64
+    N = 2 * C
+    S = 2 ** 19
+    case = signals.make_case(C, S, seed=23, pulses_per_ch=6.0)
+    thr = quiet_thresholds(C, 2 ** 18, 23)
+    G = 2 ** 18 // 4
+    splits = [0, 3 * G + 5 * N, 3 * G + 6 * N, 2 ** 18 + N, S]
+    compare(case, thr, splits, max_chunk=2 ** 18, front='split')
+    compare(case, thr, [0, S], mode=2, max_chunk=2 ** 18, front='split')
+    compare(case, thr, splits, max_chunk=2 ** 18)  # fused: plain max_chunk sub-chunks
 
 
 def test_deleted_channels_and_dead_time(gpu):

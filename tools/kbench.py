@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of libmkidgpu build variants in ONE process (cdna guide §5.4 rule 24).
 
-    python tools/kbench.py [--log2-samples 28] [--rounds 5] variantA.so variantB.so ...
+    python tools/kbench.py [--log2-samples 28] [--rounds 5] variantA.so variantB.so[:split] ...
 Each variant gets its own context on the same synthetic 1024-channel input (bench.py's feedline,
 calibrated); per round every variant processes the input once; per-kernel HIP-event times are
 reported as median / min over rounds.
@@ -10,6 +10,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -57,8 +58,10 @@ def main():
     d_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
 
     chans = []
-    for i, path in enumerate(args.libs):
-        ch = Channelizer(C, max_chunk=S, sample_rate=fs, lib_path=os.path.abspath(path))
+    for i, spec in enumerate(args.libs):
+        path, _, front = spec.partition(':')  # lib.so[:split]
+        ch = Channelizer(C, max_chunk=S, sample_rate=fs, lib_path=os.path.abspath(path),
+                         front=front or 'auto')
         ch.set_bins(feed['dds']['bins'])
         ch.set_lpf(lpf)
         ch.set_fir(np.tile(mf, (C, 1)))
@@ -86,9 +89,17 @@ def main():
                 continue  # warm-up round
             for k, (ms, n) in t.items():
                 times[path].setdefault(k, []).append(ms)
+        for path, ch in zip(args.libs, chans):  # whole pass without per-kernel events
+            ch.reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ch.process_device(x, S, phase, d_ev, cap, d_cnt)
+            torch.cuda.synchronize()
+            if r:
+                times[path].setdefault('wall', []).append((time.perf_counter() - t0) * 1e3)
     out = {}
     for path in args.libs:
-        out[os.path.basename(path)] = {k: dict(median=float(np.median(v)), min=float(np.min(v)))
+        out[os.path.basename(path).replace('.so', '')] = {k: dict(median=float(np.median(v)), min=float(np.min(v)))
                                        for k, v in times[path].items()}
     print(json.dumps(dict(samples=S, channels=C, rounds=args.rounds, kernels_ms=out), indent=1))
 

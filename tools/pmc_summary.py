@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Summarise tools/profile.sh output: per-kernel mean counter value per dispatch.
+
+    python tools/pmc_summary.py gpurun_out/prof_TAG [--json profiles/pmc_traffic.json]
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3 KiB; HBM bytes per launch = 2 x FETCH_SIZE (gfx950 counts
+half of a wide coalesced read, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both x 1024. The PMC passes
+run bench.py on a 2^28-sample step; bench.py scales `traffic` to its own launch size.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+KEEP = ('k_channelize', 'k_lpf_phase', 'k_trig_spec', 'k_trig_fix', 'k_scan_counts', 'k_gather_events')
+
+
+def short(name):
+    for k in KEEP:
+        if k in name:
+            return k
+    return None
+
+
+def read(d):
+    per = defaultdict(lambda: defaultdict(dict))  # kernel -> counter -> dispatch -> value
+    grid = {}
+    for f in glob.glob(os.path.join(d, '*', 'run_counter_collection.csv')):
+        for row in csv.DictReader(open(f)):
+            k = short(row['Kernel_Name'])
+            if not k:
+                continue
+            key = (os.path.basename(os.path.dirname(f)), row['Dispatch_Id'])
+            c = per[k][row['Counter_Name']]
+            c[key] = c.get(key, 0.0) + float(row['Counter_Value'])
+            grid[k] = int(row['Grid_Size'])
+    out = {}
+    for k, cs in per.items():
+        out[k] = {c: sum(v.values()) / len(v) for c, v in cs.items()}
+        out[k]['grid'] = grid[k]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('dir')
+    ap.add_argument('--json')
+    ap.add_argument('--samples-log2', type=int, default=28, help='ADC samples per launch in the PMC run')
+    a = ap.parse_args()
+    s = read(a.dir)
+    res = {}
+    for k, c in sorted(s.items()):
+        line = {n: round(v, 1) for n, v in sorted(c.items())}
+        if 'FETCH_SIZE' in c and 'WRITE_SIZE' in c:
+            hbm = (2 * c['FETCH_SIZE'] + c['WRITE_SIZE']) * 1024
+            line['hbm_bytes_per_launch'] = hbm
+            line['hbm_bytes_per_sample'] = hbm / (1 << a.samples_log2)
+        if 'SQ_WAVE_CYCLES' in c:
+            w = c['SQ_WAVE_CYCLES']
+            for n in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_ACTIVE_INST_VALU',
+                      'SQ_WAIT_INST_LDS'):
+                if n in c:
+                    line[n + '/WAVE_CYCLES'] = round(c[n] / w, 3)
+        res[k] = line
+        print(k, json.dumps(line))
+    if a.json:
+        out = {k: {'hbm_bytes_per_launch': v.get('hbm_bytes_per_launch'),
+                   'hbm_bytes_per_sample': v.get('hbm_bytes_per_sample'),
+                   'pmc_samples': 1 << a.samples_log2, 'source': a.dir}
+               for k, v in res.items() if 'hbm_bytes_per_launch' in v}
+        json.dump(out, open(a.json, 'w'), indent=1)
+
+
+if __name__ == '__main__':
+    main()

@@ -86,38 +86,40 @@ __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 template <int N>
 constexpr int lds_frame_elems() { return N + N / 16; }
 
+// LDS layouts of an exchange buffer: float2 index i lives at i + (i >> SH) * MUL. Pad16 (one pad
+// per 16) is the default; other exchanges pick the layout that makes both their write and their
+// read pattern bank-conflict-free (tools/lds_layouts.py checks candidates against the gfx950
+// ds_read_b64 / ds_write_b64 banking of MI355X_MICROARCH.md §LDS).
+template <int SH, int MUL>
+struct LPad {
+    __device__ __forceinline__ static constexpr int f(int i) { return i + (i >> SH) * MUL; }
+    static constexpr int size(int n) { return n + ((n - 1) >> SH) * MUL + 1; }
+};
+using Pad16 = LPad<4, 1>;
+
 // Stockham pass pieces; thread t of NT = N/PTS threads holds PTS points = PTS/R butterflies.
-// Every LDS address is one per-thread base + a compile-time offset (lpad(i + 16k) = lpad(i) +
-// 17k), so the compiler keeps one address VGPR per butterfly instead of one per point.
-template <int N, int PTS, int R>
+// Every LDS address is one per-thread base + a compile-time offset: the layouts are linear over
+// the offsets each pass adds (multiples of 2^SH for reads; r NS for writes, checked per plan by
+// tools/lds_layouts.py), so the compiler keeps one address VGPR per butterfly, not per point.
+template <int N, int PTS, int R, typename PAD = Pad16>
 __device__ __forceinline__ void st_read(const float2* buf, float2 (&v)[PTS], int t) {
     constexpr int NT = N / PTS, NB = PTS / R, NR = N / R;
-    static_assert(NT % 16 == 0 && NR % 16 == 0, "pad-linear offsets");
-    const float2* b = buf + lpad(t);
+    const float2* b = buf + PAD::f(t);
 #pragma unroll
     for (int q = 0; q < NB; ++q)
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[q * R + r] = b[(q * NT + r * NR) / 16 * 17];
+        for (int r = 0; r < R; ++r) v[q * R + r] = b[PAD::f(q * NT + r * NR)];
 }
 
-// lpad(base + r NS) - lpad(base) for the bases a Stockham write produces (base mod 16 < 8 when
-// NS == 8 and NS R >= 16; base mod 16 in {0, 4, 8, 12} when NS == 1).
-template <int NS, int R>
-__device__ __forceinline__ constexpr int st_woff(int r) {
-    static_assert(NS % 16 == 0 || (NS == 8 && NS * R >= 16) || (NS == 1 && R <= 8 && R % 4 == 0),
-                  "pad-linear write offsets");
-    return NS % 16 == 0 ? r * NS / 16 * 17 : (NS == 8 ? 8 * r + (r >> 1) : r);
-}
-
-template <int N, int PTS, int R, int NS>
+template <int N, int PTS, int R, int NS, typename PAD = Pad16>
 __device__ __forceinline__ void st_write(float2* buf, const float2 (&v)[PTS], int t) {
     constexpr int NT = N / PTS, NB = PTS / R;
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
         const int j = t + q * NT;
-        float2* b = buf + lpad((j / NS) * NS * R + (j % NS));
+        float2* b = buf + PAD::f((j / NS) * NS * R + (j % NS));
 #pragma unroll
-        for (int r = 0; r < R; ++r) b[st_woff<NS, R>(r)] = v[q * R + r];
+        for (int r = 0; r < R; ++r) b[PAD::f(r * NS)] = v[q * R + r];
     }
 }
 

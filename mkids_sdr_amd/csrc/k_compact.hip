@@ -3,26 +3,79 @@
 
 namespace mkid {
 
-// ---- compaction: exclusive scan of (channel, segment) counts (one block), then copy ----------
+// ---- compaction: exclusive scan of (channel, segment) packet counts, then copy -------------
+// Three launches, all coalesced: (1) per-tile sums of TILE consecutive entries, (2) one block
+// scans the tile sums (and accumulates the call's totals), (3) per tile: block-local exclusive
+// scan + tile offset, each thread copies the packets of its EPT entries.
+constexpr int kCmpThreads = 256;
+constexpr int kCmpEpt = 8;                       // entries per thread
+constexpr int kCmpTile = kCmpThreads * kCmpEpt;  // entries per tile
 constexpr int kScanThreads = 1024;
+
+__device__ __forceinline__ void load_counts(const int32_t* counts, int64_t n_ent, int64_t e0,
+                                            int32_t capseg, int (&v)[kCmpEpt], int64_t& raw,
+                                            int64_t& kept) {
+    raw = 0;
+    kept = 0;
+#pragma unroll
+    for (int i = 0; i < kCmpEpt; ++i) {
+        const int x = e0 + i < n_ent ? counts[e0 + i] : 0;
+        raw += x;
+        v[i] = x < capseg ? x : capseg;
+        kept += v[i];
+    }
+}
+
+// block-wide exclusive scan of one int64 per thread (kCmpThreads), returns the block total
+__device__ __forceinline__ int64_t block_excl_scan(int64_t x, int64_t& excl) {
+    __shared__ int64_t sm[kCmpThreads];
+    const int t = threadIdx.x;
+    sm[t] = x;
+    __syncthreads();
+    for (int off = 1; off < kCmpThreads; off <<= 1) {  // Hillis-Steele
+        const int64_t y = t >= off ? sm[t - off] : 0;
+        __syncthreads();
+        sm[t] += y;
+        __syncthreads();
+    }
+    excl = sm[t] - x;
+    const int64_t tot = sm[kCmpThreads - 1];
+    __syncthreads();
+    return tot;
+}
+
+__global__ __launch_bounds__(kCmpThreads) void k_tile_sums(const int32_t* counts, int64_t n_ent,
+                                                           int32_t capseg, int64_t* tile_kept,
+                                                           int64_t* tile_raw) {
+    int v[kCmpEpt];
+    int64_t raw, kept, ex;
+    const int64_t e0 = (int64_t)blockIdx.x * kCmpTile + (int64_t)threadIdx.x * kCmpEpt;
+    load_counts(counts, n_ent, e0, capseg, v, raw, kept);
+    const int64_t tk = block_excl_scan(kept, ex);
+    const int64_t tr = block_excl_scan(raw, ex);
+    if (threadIdx.x == 0) {
+        tile_kept[blockIdx.x] = tk;
+        tile_raw[blockIdx.x] = tr;
+    }
+}
 
 // d_counts[0] accumulates packets produced, d_counts[1] packets stored in `out` (<= cap), over
 // the sub-chunks of one process call (zeroed by the caller at the start of the call).
-__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* counts, int64_t n_ent,
-                                                              int32_t capseg, int64_t cap,
-                                                              int64_t* offs, int64_t* d_counts) {
+__global__ __launch_bounds__(kScanThreads) void k_tile_scan(const int64_t* tile_kept, const int64_t* tile_raw,
+                                                            int64_t ntiles, int64_t cap, int64_t* tile_off,
+                                                            int64_t* d_counts) {
     __shared__ int64_t part[kScanThreads];
     __shared__ unsigned long long tot;
     const int64_t prev = d_counts[1];
-    const int64_t per = (n_ent + kScanThreads - 1) / kScanThreads;
+    const int64_t per = (ntiles + kScanThreads - 1) / kScanThreads;
     const int64_t b = threadIdx.x * per;
     int64_t sum = 0, sumw = 0;
     for (int64_t i = 0; i < per; ++i)
-        if (b + i < n_ent) { const int v = counts[b + i]; sum += v; sumw += v < capseg ? v : capseg; }
+        if (b + i < ntiles) { sum += tile_raw[b + i]; sumw += tile_kept[b + i]; }
     part[threadIdx.x] = sumw;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
-    for (int off = 1; off < kScanThreads; off <<= 1) {  // Hillis-Steele inclusive scan
+    for (int off = 1; off < kScanThreads; off <<= 1) {
         const int64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
         __syncthreads();
         part[threadIdx.x] += v;
@@ -30,7 +83,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* cou
     }
     int64_t run = prev + part[threadIdx.x] - sumw;
     for (int64_t i = 0; i < per; ++i)
-        if (b + i < n_ent) { offs[b + i] = run; const int v = counts[b + i]; run += v < capseg ? v : capseg; }
+        if (b + i < ntiles) { tile_off[b + i] = run; run += tile_kept[b + i]; }
     atomicAdd(&tot, (unsigned long long)sum);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -40,27 +93,42 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* cou
     }
 }
 
-__global__ __launch_bounds__(256) void k_gather_events(const uint64_t* slots, const int32_t* counts,
-                                                       int64_t n_ent, int32_t capseg,
-                                                       const int64_t* offs, uint64_t* out,
-                                                       int64_t cap) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n_ent) return;
-    const int n = counts[e] < capseg ? counts[e] : capseg;
-    const int64_t o = offs[e];
-    for (int i = 0; i < n; ++i)
-        if (o + i < cap) out[o + i] = slots[e * capseg + i];
+__global__ __launch_bounds__(kCmpThreads) void k_gather_events(const uint64_t* slots, const int32_t* counts,
+                                                               int64_t n_ent, int32_t capseg,
+                                                               const int64_t* tile_off, uint64_t* out,
+                                                               int64_t cap) {
+    int v[kCmpEpt];
+    int64_t raw, kept, ex;
+    const int64_t e0 = (int64_t)blockIdx.x * kCmpTile + (int64_t)threadIdx.x * kCmpEpt;
+    load_counts(counts, n_ent, e0, capseg, v, raw, kept);
+    block_excl_scan(kept, ex);
+    int64_t o = tile_off[blockIdx.x] + ex;
+#pragma unroll
+    for (int i = 0; i < kCmpEpt; ++i) {
+        const uint64_t* src = slots + (e0 + i) * capseg;
+        for (int k = 0; k < v[i]; ++k)
+            if (o + k < cap) out[o + k] = src[k];
+        o += v[i];
+    }
 }
 
 hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
                           int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
                           int64_t* scan_ws, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, s, counts, n_ent, capseg,
-                       cap, scan_ws, d_counts);
+    // scan_ws holds n_ent int64 (>= 3 per tile)
+    const int64_t ntiles = (n_ent + kCmpTile - 1) / kCmpTile;
+    int64_t* tile_kept = scan_ws;
+    int64_t* tile_raw = scan_ws + ntiles;
+    int64_t* tile_off = scan_ws + 2 * ntiles;
+    hipLaunchKernelGGL(k_tile_sums, dim3((unsigned)ntiles), dim3(kCmpThreads), 0, s, counts, n_ent, capseg,
+                       tile_kept, tile_raw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gather_events, dim3((unsigned)((n_ent + 255) / 256)), dim3(256), 0, s,
-                       slots, counts, n_ent, capseg, scan_ws, out, cap);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, s, tile_kept, tile_raw, ntiles, cap,
+                       tile_off, d_counts);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gather_events, dim3((unsigned)ntiles), dim3(kCmpThreads), 0, s, slots, counts, n_ent,
+                       capseg, tile_off, out, cap);
     return hipGetLastError();
 }
 

@@ -8,7 +8,9 @@
 //   input  LDS ring of RS = 2T-1+FPB hops of M int16 I/Q samples; each iteration brings 4 new
 //          hops with ONE 16-byte global load per thread, issued one iteration ahead.
 //   PFB    u[p] = sum_tau h[tau N + p] x[(k+1)M - TN + tau N + p]   (h as float4 per p in LDS)
-//   FFT    Stockham radix-8/4 passes through a padded per-frame LDS buffer (fft_common.h).
+//   FFT    Stockham radix-8/4 passes through a padded per-frame LDS buffer (fft_common.h); the
+//          last pass is fused into the select: thread c evaluates only the radix-4 butterfly
+//          output X[bin_c] (4 LDS reads, 3 complex MACs with per-channel constant twiddles).
 //   DDC    thread c = channel c: z_k = X_k[bin_c] (-1)^(bin_c (k+1)) conj(LUT_c[k mod P]) / 2^15
 //          for the 4 frames of the iteration (LO table [P][C]: one contiguous row per frame).
 //   LPF    transposed form, 13 complex accumulators per thread: frame 2j adds g_{2m+1} z to
@@ -24,17 +26,33 @@
 
 namespace mkid {
 
+// Radix sequence per FFT length (8 points per thread). The last pass is not run through LDS:
+// its radix-RL butterfly is evaluated only for the selected bin, by the channel's thread.
+template <int N>
+struct FPlan;
+template <> struct FPlan<128>  { static constexpr int NP = 3, R[4] = {8, 4, 4, 1}; };
+template <> struct FPlan<256>  { static constexpr int NP = 3, R[4] = {8, 8, 4, 1}; };
+template <> struct FPlan<512>  { static constexpr int NP = 4, R[4] = {8, 4, 4, 4}; };
+template <> struct FPlan<1024> { static constexpr int NP = 4, R[4] = {8, 8, 4, 4}; };
+template <> struct FPlan<2048> { static constexpr int NP = 4, R[4] = {8, 8, 8, 4}; };
+
 template <int N>
 struct FGeo {
     static constexpr int PTS = 8, NT = N / PTS, FPB = 4;
     static constexpr int BT = NT * FPB;                 // == C: one channel per thread
     static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
     static constexpr int RS = 2 * T - 1 + FPB;          // ring slots (hops)
-    static constexpr int LDSF = lds_frame_elems<N>();
+    // exchange B (pass-2 write -> pass-3 read; plans with 4 passes) layout: conflict-free at
+    // N >= 1024, half the read cycles of Pad16 at N = 512 (tools/lds_layouts.py)
+    using PadB = LPad<5, 4>;
+    static constexpr int LDSF = (Pad16::size(N) > PadB::size(N) ? Pad16::size(N) : PadB::size(N)) + 1 & ~1;
     static constexpr int SPT = FPB * M / BT;            // new samples per thread per iteration
     static_assert(SPT == 4, "one 16-byte load per thread per iteration");
     static_assert(BT == C, "one channel per thread");
-    static constexpr int NS2 = Plan8<N>::R[0], NS3 = NS2 * Plan8<N>::R[1], NS4 = NS3 * Plan8<N>::R[2];
+    static constexpr int NS2 = FPlan<N>::R[0], NS3 = NS2 * FPlan<N>::R[1];
+    static constexpr int RL = FPlan<N>::R[FPlan<N>::NP - 1];  // radix of the fused last pass
+    static constexpr int NSL = N / RL;                        // its butterfly count / stride
+    static_assert(NSL % 16 == 0, "pad-linear offsets in the fused last pass");
     static constexpr size_t lds_bytes = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8 + (size_t)N * 16;
     static constexpr int HIST = (2 * T - 1 + kLpfHist) * M;  // ADC history samples
     // register budget sized for 4 waves per SIMD (16 per CU, <= 128 VGPRs): HIP's second
@@ -55,7 +73,7 @@ __device__ __forceinline__ uint4 front_load(const FrontArgs& a, int64_t first_ho
 template <int N>
 __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs a) {
     using G = FGeo<N>;
-    using PL = Plan8<N>;
+    using PL = FPlan<N>;
     constexpr int PTS = G::PTS, NT = G::NT, M = G::M, C = G::C, T = G::T, RS = G::RS, FPB = G::FPB;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
@@ -74,15 +92,25 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
 
     TwiddleRec<N, PTS, PL::R[1], G::NS2> tw2;
     tw2.init(t);
-    TwiddleRec<N, PTS, PL::R[2], G::NS3> tw3;
-    tw3.init(t);
-    TwiddleRec<N, PTS, (PL::NP == 4 ? PL::R[3] : 2), G::NS4> tw4;
-    if constexpr (PL::NP == 4) tw4.init(t);
+    TwiddleRec<N, PTS, (PL::NP == 4 ? PL::R[2] : 2), G::NS3> tw3;
+    if constexpr (PL::NP == 4) tw3.init(t);
 
     const int c = tid;  // channel of the select / low-pass / phase stage
     const int32_t bin = a.bins[c];
     const float ic = a.ic[c], qc = a.qc[c];
     const int podd_mask = bin & 1;
+    // fused last pass for X[bin]: bin = jl + NSL s,
+    //   X[bin] = sum_r W_RL^{r s} W_N^{jl r} Y[jl + r NSL]   (Stockham last pass, NS = NSL)
+    constexpr int RL = G::RL, NSL = G::NSL;
+    const int jl = bin % NSL, sl = bin / NSL;
+    float2 tl[RL - 1];
+#pragma unroll
+    for (int r = 1; r < RL; ++r) {
+        double sn, cs;
+        sincospi(-2.0 * ((double)(jl * r) / N + (double)((r * sl) % RL) / RL), &sn, &cs);
+        tl[r - 1] = make_float2((float)cs, (float)sn);
+    }
+    const int yoff = lpad(jl);
 
     const int64_t k_b = (int64_t)blockIdx.x * a.frames_per_block;
     int64_t k_e = k_b + a.frames_per_block;
@@ -150,20 +178,17 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         __syncthreads();
         tw2.apply(v);
         st_dft<PTS, PL::R[1]>(v);
-        st_write<N, PTS, PL::R[1], G::NS2>(buf, v, t);
-        __syncthreads();
-        st_read<N, PTS, PL::R[2]>(buf, v, t);
-        __syncthreads();
-        tw3.apply(v);
-        st_dft<PTS, PL::R[2]>(v);
-        st_write<N, PTS, PL::R[2], G::NS3>(buf, v, t);
-        __syncthreads();
         if constexpr (PL::NP == 4) {
-            st_read<N, PTS, PL::R[3]>(buf, v, t);
+            st_write<N, PTS, PL::R[1], G::NS2, typename G::PadB>(buf, v, t);
             __syncthreads();
-            tw4.apply(v);
-            st_dft<PTS, PL::R[3]>(v);
-            st_write<N, PTS, PL::R[3], G::NS4>(buf, v, t);
+            st_read<N, PTS, PL::R[2], typename G::PadB>(buf, v, t);
+            __syncthreads();
+            tw3.apply(v);
+            st_dft<PTS, PL::R[2]>(v);
+            st_write<N, PTS, PL::R[2], G::NS3>(buf, v, t);
+            __syncthreads();
+        } else {
+            st_write<N, PTS, PL::R[1], G::NS2>(buf, v, t);
             __syncthreads();
         }
 
@@ -171,7 +196,14 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
 #pragma unroll
         for (int f = 0; f < FPB; ++f) {
             const int64_t k = kb + f;
-            float2 X = fbuf[f * G::LDSF + lpad(bin)];
+            const float2* yf = fbuf + f * G::LDSF + yoff;
+            float2 X = yf[0];
+#pragma unroll
+            for (int r = 1; r < RL; ++r) {
+                const float2 yv = yf[r * NSL / 16 * 17];
+                X.x = fmaf(tl[r - 1].x, yv.x, fmaf(-tl[r - 1].y, yv.y, X.x));
+                X.y = fmaf(tl[r - 1].x, yv.y, fmaf(tl[r - 1].y, yv.x, X.y));
+            }
             if ((int)((a.k0 + k + 1) & 1) & podd_mask) X = make_float2(-X.x, -X.y);
             const float2 z = cmul(X, lov[f]);
             if ((f & 1) == 0) {  // frame 2j: taps 1,3,..,25 into outputs j..j+12

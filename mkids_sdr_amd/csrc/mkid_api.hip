@@ -287,7 +287,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_ysum, C);
     AL(d_slots, (size_t)c->slot_cap);
     AL(d_chcounts, (size_t)C * c->nseg_max);
-    AL(d_scan, (size_t)C * c->nseg_max);
+    AL(d_scan, (size_t)C * c->nseg_max + 64);  // >= 3 int64 per compaction tile
     AL(d_sspec, (size_t)C * c->nseg_max);
     AL(d_send, (size_t)C * c->nseg_max);
     AL(d_scratch, (size_t)C * c->scratch_cap);

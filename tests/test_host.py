@@ -2,6 +2,8 @@
 LUT synthesis, register codecs, the FpgaClient register shim and the ChannelizerControls
 mirror driving it (no GPU: the shim's data path is not touched)."""
 import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 import struct
 
 import numpy as np
@@ -177,3 +179,19 @@ def test_replay_triggers_restated():
     h2 = replay.block_mean_trigger(x, averagelength=128, start=100, need=300, skip=200,
                                    wrap_negative=False)
     assert h2[0] == 3000 and 3500 in h2
+
+
+def test_lds_layouts_linear():
+    """st_read/st_write use base + compile-time offsets: every layout/pass pair must be linear
+    (a wrong layout would silently scramble the FFT)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import lds_layouts as L
+    for N in L.FRONT_PLANS:
+        for name, Rw, NS, Rr, p in L.front_exchanges(N):
+            assert L.exchange(N, Rw, NS, Rr, p)[0], ('k_front', N, name)
+    for N in L.CHAN_PLANS:
+        for name, Rw, NS, Rr, p in L.chan_exchanges(N):
+            assert L.exchange(N, Rw, NS, Rr, p)[0], ('k_channelize', N, name)
+    # the conflict-free claim for the headline geometry
+    assert L.exchange(2048, 8, 8, 8, L.PADB)[1:] == (32, 16)

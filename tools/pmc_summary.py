@@ -14,7 +14,8 @@ import json
 import os
 from collections import defaultdict
 
-KEEP = ('k_channelize', 'k_lpf_phase', 'k_trig_spec', 'k_trig_fix', 'k_scan_counts', 'k_gather_events')
+KEEP = ('k_front', 'k_channelize', 'k_lpf_phase', 'k_trig_spec', 'k_trig_fix', 'k_tile_sums', 'k_tile_scan',
+        'k_gather_events')
 
 
 def short(name):
@@ -32,13 +33,17 @@ def read(d):
             k = short(row['Kernel_Name'])
             if not k:
                 continue
-            key = (os.path.basename(os.path.dirname(f)), row['Dispatch_Id'])
+            g = int(row['Grid_Size'])
+            key = (os.path.basename(os.path.dirname(f)), row['Dispatch_Id'], g)
             c = per[k][row['Counter_Name']]
             c[key] = c.get(key, 0.0) + float(row['Counter_Value'])
-            grid[k] = int(row['Grid_Size'])
+            grid[k] = max(grid.get(k, 0), g)
     out = {}
-    for k, cs in per.items():
-        out[k] = {c: sum(v.values()) / len(v) for c, v in cs.items()}
+    for k, cs in per.items():  # only the largest launches (the timed step, not calibration)
+        out[k] = {}
+        for c, v in cs.items():
+            vals = [x for key, x in v.items() if key[2] == grid[k]]
+            out[k][c] = sum(vals) / len(vals)
         out[k]['grid'] = grid[k]
     return out
 

@@ -24,6 +24,27 @@
 #include "fft_common.h"
 #include "mkid_internal.h"
 
+// MKID_XP_STAMPS (timing experiments only, tools/stamps.py): lane 0 of every wave of the first
+// 4 workgroups records s_memtime before and after each barrier of iterations 8..15 into the
+// phase buffer (which then holds no phases).
+#ifdef MKID_XP_STAMPS
+#define FSYNC(id)                  \
+    do {                           \
+        STAMP(2 * (id));           \
+        __syncthreads();           \
+        STAMP(2 * (id) + 1);       \
+    } while (0)
+#define STAMP(slot_)                                                                              \
+    do {                                                                                          \
+        if (blockIdx.x < 4 && it_ >= 8 && it_ < 16 && (threadIdx.x & 63) == 0)                   \
+            reinterpret_cast<uint64_t*>(a.phase)[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 +   \
+                                                  (it_ - 8)) * 16 + (slot_)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define FSYNC(id) __syncthreads()
+#define STAMP(slot_) ((void)0)
+#endif
+
 namespace mkid {
 
 // Radix sequence per FFT length (8 points per thread). The last pass is not run through LDS:
@@ -136,7 +157,14 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     for (int m = 0; m < 13; ++m) acc[m] = make_float2(0.f, 0.f);
     float2 ys = make_float2(0.f, 0.f);
 
+#ifdef MKID_XP_STAMPS
+    int it_ = 0;
+#endif
     for (int64_t kb = k_start; kb < k_e; kb += FPB) {
+#ifdef MKID_XP_STAMPS
+        ++it_;
+        STAMP(14);
+#endif
         // LO rows of this iteration's frames (latency hidden behind the FFT)
         float2 lov[FPB];
 #pragma unroll
@@ -166,30 +194,30 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
             asm volatile("" : "+v"(v[r].x), "+v"(v[r].y));
         }
         st_dft<PTS, PL::R[0]>(v);
-        __syncthreads();  // ring reads of this iteration and last iteration's select are done
+        FSYNC(0);  // ring reads of this iteration and last iteration's select are done
         {
             const int64_t hop = kb + FPB + (tid * G::SPT) / M;
             *reinterpret_cast<uint4*>(ring + (int)(((hop % RS) + RS) % RS) * M + (tid * G::SPT) % M) = pre;
             pre = front_load<N>(a, kb + 2 * FPB, tid);
         }
         st_write<N, PTS, PL::R[0], 1>(buf, v, t);
-        __syncthreads();
+        FSYNC(1);
         st_read<N, PTS, PL::R[1]>(buf, v, t);
-        __syncthreads();
+        FSYNC(2);
         tw2.apply(v);
         st_dft<PTS, PL::R[1]>(v);
         if constexpr (PL::NP == 4) {
             st_write<N, PTS, PL::R[1], G::NS2, typename G::PadB>(buf, v, t);
-            __syncthreads();
+            FSYNC(3);
             st_read<N, PTS, PL::R[2], typename G::PadB>(buf, v, t);
-            __syncthreads();
+            FSYNC(4);
             tw3.apply(v);
             st_dft<PTS, PL::R[2]>(v);
             st_write<N, PTS, PL::R[2], G::NS3>(buf, v, t);
-            __syncthreads();
+            FSYNC(5);
         } else {
             st_write<N, PTS, PL::R[1], G::NS2>(buf, v, t);
-            __syncthreads();
+            FSYNC(6);
         }
 
         // ---- select + DDC + low-pass + phase for channel c over the FPB frames ----
@@ -229,7 +257,9 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
                     const float ph = atan2f(y.y - qc, y.x - ic);
                     int q = __float2int_rn(ph * 8192.0f);
                     q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
+#ifndef MKID_XP_STAMPS
                     if (a.phase) a.phase[j * C + c] = ph;
+#endif
                     a.raw[j * C + c] = (int16_t)q;
                 }
             }

@@ -36,9 +36,12 @@
     } while (0)
 #define STAMP(slot_)                                                                              \
     do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        const uint64_t tm_ = __builtin_amdgcn_s_memtime();                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
         if (blockIdx.x < 4 && it_ >= 8 && it_ < 16 && (threadIdx.x & 63) == 0)                   \
             reinterpret_cast<uint64_t*>(a.phase)[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 +   \
-                                                  (it_ - 8)) * 16 + (slot_)] = __builtin_amdgcn_s_memtime(); \
+                                                  (it_ - 8)) * 16 + (slot_)] = tm_;               \
     } while (0)
 #else
 #define FSYNC(id) __syncthreads()
@@ -138,6 +141,9 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     if (k_e > a.K) k_e = a.K;
     if (k_b >= k_e) return;
     const int64_t k_start = k_b - kLpfHist;  // warm-up frames rebuild the low-pass history
+    // outputs of this run: rows j = k_b/2 .. ; 32-bit offsets from per-run bases
+    int16_t* const raw_run = a.raw + (k_b >> 1) * C;
+    [[maybe_unused]] float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
 
     // prologue: hops k_start-2T+1 .. k_start+FPB-1 -> ring (slot = hop mod RS)
     {
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         // LO rows of this iteration's frames (latency hidden behind the FFT)
         float2 lov[FPB];
 #pragma unroll
-        for (int f = 0; f < FPB; ++f) lov[f] = a.lo[(int64_t)((a.k0 + kb + f) & (a.P - 1)) * C + c];
+        for (int f = 0; f < FPB; ++f) lov[f] = a.lo[((int)(a.k0 + kb + f) & (a.P - 1)) * C + c];
 
         // ---- PFB of frame kb + slot from the LDS ring ----
         const int64_t h_first = kb + slot + 1 - 2 * T;
@@ -191,7 +197,10 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
             }
             v[r] = make_float2(ur, ui);
             // keep the point order: stops the scheduler from hoisting all 32 ring loads at once
-            asm volatile("" : "+v"(v[r].x), "+v"(v[r].y));
+            // (register pressure) ...
+            if ((r & 3) == 3)  // ... but let four points' loads overlap
+                asm volatile("" : "+v"(v[r].x), "+v"(v[r].y), "+v"(v[r - 1].x), "+v"(v[r - 1].y),
+                             "+v"(v[r - 2].x), "+v"(v[r - 2].y), "+v"(v[r - 3].x), "+v"(v[r - 3].y));
         }
         st_dft<PTS, PL::R[0]>(v);
         FSYNC(0);  // ring reads of this iteration and last iteration's select are done
@@ -234,6 +243,13 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
             }
             if ((int)((a.k0 + k + 1) & 1) & podd_mask) X = make_float2(-X.x, -X.y);
             const float2 z = cmul(X, lov[f]);
+#ifdef MKID_XP_STAMPS
+            if (f == 0) {
+                asm volatile("" ::"v"(z.x), "v"(z.y));
+                STAMP(12);  // frame 0 selected (its LDS reads and LO load have landed)
+            }
+            if (f == 2) STAMP(13);  // output 0 written
+#endif
             if ((f & 1) == 0) {  // frame 2j: taps 1,3,..,25 into outputs j..j+12
 #pragma unroll
                 for (int m = 0; m < 13; ++m) {
@@ -251,16 +267,16 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
                 for (int m = 0; m < 12; ++m) acc[m] = acc[m + 1];
                 acc[12] = make_float2(0.f, 0.f);
                 if (k > k_b && k < k_e) {
-                    const int64_t j = (k - 1) >> 1;
+                    const int jr = (int)((k - 1 - k_b) >> 1);  // row within the run
                     ys.x += y.x;
                     ys.y += y.y;
-                    const float ph = atan2f(y.y - qc, y.x - ic);
+                    const float ph = phase_atan2(y.y - qc, y.x - ic);
                     int q = __float2int_rn(ph * 8192.0f);
                     q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
 #ifndef MKID_XP_STAMPS
-                    if (a.phase) a.phase[j * C + c] = ph;
+                    if (phase_run) phase_run[jr * C + c] = ph;
 #endif
-                    a.raw[j * C + c] = (int16_t)q;
+                    raw_run[jr * C + c] = (int16_t)q;
                 }
             }
         }

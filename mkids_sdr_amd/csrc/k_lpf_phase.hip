@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
                 }
                 ys.x += yr;
                 ys.y += yi;
-                const float ph = atan2f(yi - qc, yr - ic);
+                const float ph = phase_atan2(yi - qc, yr - ic);
                 int q = __float2int_rn(ph * 8192.0f);
                 q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
                 if (a.phase) a.phase[j * C + c] = ph;

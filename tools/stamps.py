@@ -22,7 +22,8 @@ SEG = [('PFB (ring reads, taps, FMA, dft8)', 14, 0), ('wait S0', 0, 1),
        ('pass-2 twiddle+dft8+write', 5, 6), ('wait S3', 6, 7),
        ('pass-3 read', 7, 8), ('wait S4', 8, 9),
        ('pass-3 twiddle+dft8+write', 9, 10), ('wait S5', 10, 11),
-       ('select+DDC+LPF+atan+stores', 11, 'next14')]
+       ('select frame 0 (LDS reads, LO load)', 11, 12), ('frames 0-1 LPF + output 0', 12, 13),
+       ('frames 2-3 + output 1 + loop', 13, 'next14')]
 
 
 def main():

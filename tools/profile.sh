@@ -3,7 +3,7 @@
 #   bash tools/profile.sh TAG
 # 1. kernel trace + stats of the default bench workload (per-kernel average durations);
 # 2. PMC passes, each its own run (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950;
-#    counters are never combined with runtime/sys traces), on a 2^28-sample step.
+#    counters are never combined with runtime/sys traces), on one default (2^30-sample) step.
 # Output: gpurun_out/prof_TAG/{kt,fetch,write,sq1,sq2}/...
 set -euo pipefail
 TAG=${1:-run}
@@ -15,7 +15,7 @@ cd /tmp
 B="python3 $ROOT/bench.py --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
     -- $B --steps 3 --warmup 1 > "$OUT/kt.log" 2>&1
-SMALL="--steps 1 --warmup 1 --log2-samples 28"
+SMALL="--steps 1 --warmup 1"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
     -- $B $SMALL > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \

@@ -142,6 +142,9 @@ int mkid_process_device(mkid_ctx* ctx, const int16_t* d_iq, int64_t nsamples, fl
  * device pointer valid until the next process call. Replaces the snapPhase_bram source
  * (ROACH_Pulses.py:357-378). */
 int mkid_last_raw_phase(mkid_ctx* ctx, const int16_t** d_raw, int64_t* nrows);
+/* Host copy of the same rows (at most cap_rows rows of C int16; *rows = rows available): the
+ * snapshot readback (conv_phase_snapPhase_bram / qdr0 longsnapshot, ROACH_Pulses.py:433-551). */
+int mkid_read_raw_phase(mkid_ctx* ctx, int16_t* host_out, int64_t cap_rows, int64_t* rows);
 
 /* Diagnostic: trigger segments of the last sub-chunk whose speculative start state had to be
  * re-run by the exact fix-up pass (0 = all speculation was right; results are exact either way). */
@@ -154,6 +157,31 @@ int mkid_avg_iq(mkid_ctx* ctx, float* mean_i, float* mean_q);
  *   [63:56] ch | [55:44] peak | [43:32] p1 = peak-base+2048 | [31:20] base | [19:0] ts mod 2^20
  * (ROACH_Pulses.py:805-832 decode; PacketMaster.c:291-292 assembly; ch 255 = end-of-second). */
 int mkid_pack_reference(const uint64_t* wide, int64_t n, uint64_t* out);
+
+/* Host-replay triggers of the reference on device phase. Input: Fix16_13
+ * phase int16 [n][ld] (e.g. mkid_last_raw_phase, or snapshots uploaded by the caller), columns
+ * 0..nch-1 are channels. Phase in degrees = raw*360/2^16*4/pi (pulse_triggering_v2.py:93-95).
+ *   MKID_REPLAY_ROLLING  pulse_triggering_v2.py:104-174: start = 100+m, need = skip = pulselength,
+ *                        length = m (meanlength, 20), |mean(x[j-m:j]) - x[j]| > threshold
+ *   MKID_REPLAY_BLOCK    pulse_triggering.py:109-208 (start 100, need 300, skip 200, wrap on) and
+ *                        ROACH_Pulses.py:614-727 (start 500): length = averagelength (2^k),
+ *                        |mean(block(j)) - x[j]| > threshold
+ * Hits (sample indices) go to d_hits[c*cap + i], i < cap; d_counts[c] = hits found (may exceed
+ * cap: then hits were dropped). Means use numpy's pairwise float64 summation order, so the hit
+ * lists equal the reference's numpy loops exactly. Runs on the context stream. */
+#define MKID_REPLAY_ROLLING 0
+#define MKID_REPLAY_BLOCK 1
+typedef struct mkid_replay_cfg {
+    int32_t mode;          /* MKID_REPLAY_ROLLING / MKID_REPLAY_BLOCK                       */
+    int32_t length;        /* rolling: meanlength m; block: averagelength A                 */
+    int32_t start;         /* first index tested ("bob")                                    */
+    int32_t need;          /* stop when bob + need > n                                      */
+    int32_t skip;          /* advance after a hit                                           */
+    int32_t wrap_negative; /* add 360 deg to negative phase first (pulse_triggering.py:110)  */
+    double threshold_deg;  /* strict: |mean - x| > threshold                                */
+} mkid_replay_cfg;
+int mkid_replay_trigger(mkid_ctx* ctx, const int16_t* d_raw, int64_t n, int64_t ld, int32_t nch,
+                        const mkid_replay_cfg* cfg, int32_t* d_hits, int32_t cap, int32_t* d_counts);
 
 /* Kernel timing with HIP events on the context stream (for bench roofline numbers). */
 #define MKID_K_CHANNELIZE 0

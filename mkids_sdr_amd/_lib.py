@@ -42,6 +42,15 @@ class Cfg(ctypes.Structure):
                 ('max_chunk', ctypes.c_int64), ('sample_rate', ctypes.c_double)]
 
 
+REPLAY_ROLLING, REPLAY_BLOCK = 0, 1
+
+
+class ReplayCfg(ctypes.Structure):
+    _fields_ = [('mode', ctypes.c_int32), ('length', ctypes.c_int32), ('start', ctypes.c_int32),
+                ('need', ctypes.c_int32), ('skip', ctypes.c_int32), ('wrap_negative', ctypes.c_int32),
+                ('threshold_deg', ctypes.c_double)]
+
+
 class SynthTone(ctypes.Structure):
     _fields_ = [('amp', ctypes.c_float), ('phase0', ctypes.c_float),
                 ('freq_index', ctypes.c_int32), ('pad', ctypes.c_int32)]
@@ -71,11 +80,13 @@ _SIGS = {
     'mkid_process': [P, P, I64, P, P, I64, P],
     'mkid_process_device': [P, P, I64, P, P, I64, P],
     'mkid_last_raw_phase': [P, P, P],
+    'mkid_read_raw_phase': [P, P, I64, P],
     'mkid_avg_iq': [P, P, P],
     'mkid_trigger_reruns': [P, P],
     'mkid_pack_reference': [P, I64, P],
     'mkid_set_timing': [P, I32],
     'mkid_get_timing': [P, I32, P, P],
+    'mkid_replay_trigger': [P, P, I64, I64, I32, P, P, I32, P],
     'mkid_synth_adc': [P, P, I64, I64, P, P, P, I64, ctypes.c_float, ctypes.c_float, I32,
                        ctypes.c_float, ctypes.c_uint32],
 }

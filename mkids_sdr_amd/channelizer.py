@@ -130,6 +130,14 @@ class Channelizer:
         self._chk(self._L.mkid_last_raw_phase(self._h, ctypes.byref(p), ctypes.byref(n)))
         return p.value, n.value
 
+    def raw_phase(self):
+        """Host copy of the last sub-chunk's Fix16_13 phase rows, int16 [rows][C]."""
+        p, rows = self.raw_phase_ptr()
+        out = np.empty((rows, self.C), np.int16)
+        n = ctypes.c_int64()
+        self._chk(self._L.mkid_read_raw_phase(self._h, _ptr(out), rows, ctypes.byref(n)))
+        return out
+
     def trigger_reruns(self):
         n = ctypes.c_int64()
         self._chk(self._L.mkid_trigger_reruns(self._h, ctypes.byref(n)))
@@ -140,6 +148,23 @@ class Channelizer:
         mq = np.empty(self.C, np.float32)
         self._chk(self._L.mkid_avg_iq(self._h, _ptr(mi), _ptr(mq)))
         return mi, mq
+
+    # ---- host-replay triggers --------------------------------------------
+    def replay_trigger(self, d_raw, n, ld, nch, mode, length, start, need, skip, threshold_deg,
+                       wrap_negative=False, d_hits=None, cap=64, d_counts=None):
+        """Run the reference's rolling-/block-mean replay trigger on device Fix16_13 phase
+        d_raw[n][ld] (int16 device tensor or pointer), channels 0..nch-1. Returns the device
+        (hits [nch, cap] int32, counts [nch] int32) tensors (allocated when not given)."""
+        import torch
+        if d_hits is None:
+            d_hits = torch.full((nch, cap), -1, dtype=torch.int32, device='cuda')
+        if d_counts is None:
+            d_counts = torch.zeros(nch, dtype=torch.int32, device='cuda')
+        rc = _lib.ReplayCfg(int(mode), int(length), int(start), int(need), int(skip),
+                            1 if wrap_negative else 0, float(threshold_deg))
+        self._chk(self._L.mkid_replay_trigger(self._h, _ptr(d_raw), int(n), int(ld), int(nch),
+                                              ctypes.byref(rc), _ptr(d_hits), int(cap), _ptr(d_counts)))
+        return d_hits, d_counts
 
     # ---- timing ------------------------------------------------------------------------------
     def set_timing(self, on):

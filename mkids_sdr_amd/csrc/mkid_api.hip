@@ -83,6 +83,10 @@ struct mkid_ctx {
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
     int64_t last_J = 0;     // phase rows of the last call
     int64_t last_subJ = 0;  // rows of its last sub-chunk (held in d_raw)
+    // replay-trigger workspace (lazy, grown on demand)
+    uint32_t* d_rflags = nullptr;
+    double* d_rmeans = nullptr;
+    size_t rflags_n = 0, rmeans_n = 0;
     // host-API staging (lazy)
     uint32_t* d_in = nullptr;
     float* d_phase_ws = nullptr;
@@ -156,7 +160,7 @@ static void free_all(mkid_ctx* c) {
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
-                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns};
+                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -628,6 +632,18 @@ int mkid_last_raw_phase(mkid_ctx* c, const int16_t** d_raw, int64_t* nrows) {
     return MKID_OK;
 }
 
+int mkid_read_raw_phase(mkid_ctx* c, int16_t* host_out, int64_t cap_rows, int64_t* rows) {
+    if (!c || !rows || (cap_rows > 0 && !host_out)) return MKID_E_ARG;
+    const int64_t avail = std::min(c->last_subJ, c->Jmax);
+    *rows = avail;
+    const int64_t n = std::min(avail, cap_rows);
+    if (n <= 0) return MKID_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(host_out, c->d_raw, (size_t)n * c->C * 2, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MKID_OK;
+}
+
 int mkid_trigger_reruns(mkid_ctx* c, int64_t* total) {
     if (!c || !total) return MKID_E_ARG;
     std::vector<int32_t> r(c->C);
@@ -651,6 +667,40 @@ int mkid_avg_iq(mkid_ctx* c, float* mi, float* mq) {
         mi[i] = (float)(s[i].x / (double)c->last_J);
         mq[i] = (float)(s[i].y / (double)c->last_J);
     }
+    return MKID_OK;
+}
+
+int mkid_replay_trigger(mkid_ctx* c, const int16_t* d_raw, int64_t n, int64_t ld, int32_t nch,
+                        const mkid_replay_cfg* rc, int32_t* d_hits, int32_t cap, int32_t* d_counts) {
+    if (!c || !d_raw || !rc || !d_counts || (cap > 0 && !d_hits)) return MKID_E_ARG;
+    if (n <= 0 || nch <= 0 || ld < nch || cap < 0) FAIL(c, MKID_E_ARG, "replay: bad shape");
+    if (rc->mode != MKID_REPLAY_ROLLING && rc->mode != MKID_REPLAY_BLOCK) FAIL(c, MKID_E_ARG, "replay: bad mode");
+    if (rc->length <= 0 || rc->start < 0 || rc->need < 0 || rc->skip <= 0)
+        FAIL(c, MKID_E_ARG, "replay: length/start/need/skip out of range");
+    if (rc->mode == MKID_REPLAY_ROLLING && rc->start < rc->length)
+        FAIL(c, MKID_E_ARG, "replay: rolling start must be >= meanlength");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t nf = (size_t)nch * (size_t)((n + 31) / 32);
+    const size_t nm = rc->mode == MKID_REPLAY_BLOCK ? (size_t)nch * (size_t)(n / rc->length) : 0;
+    if (nf > c->rflags_n) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->d_rflags) HIPCHK(c, hipFree(c->d_rflags));
+        c->d_rflags = nullptr;
+        c->rflags_n = 0;
+        HIPCHK(c, dalloc(&c->d_rflags, nf));
+        c->rflags_n = nf;
+    }
+    if (nm > c->rmeans_n) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->d_rmeans) HIPCHK(c, hipFree(c->d_rmeans));
+        c->d_rmeans = nullptr;
+        c->rmeans_n = 0;
+        HIPCHK(c, dalloc(&c->d_rmeans, nm));
+        c->rmeans_n = nm;
+    }
+    HIPCHK(c, launch_replay(d_raw, n, ld, nch, rc->mode, rc->length, rc->start, rc->need, rc->skip,
+                            rc->wrap_negative, rc->threshold_deg, c->d_rflags, c->d_rmeans, d_hits, cap,
+                            d_counts, c->stream));
     return MKID_OK;
 }
 

@@ -107,6 +107,10 @@ hipError_t launch_synth(int16_t* out, int64_t n, int64_t n0, const int16_t* base
                         float tr, float tf, int32_t window, float sigma, uint32_t seed,
                         hipStream_t s);
 
+hipError_t launch_replay(const int16_t* raw, int64_t n, int64_t ld, int32_t nch, int32_t mode, int32_t length,
+                         int64_t start, int64_t need, int64_t skip, int32_t wrap, double thr, uint32_t* flags,
+                         double* means, int32_t* hits, int32_t cap, int32_t* counts, hipStream_t s);
+
 bool channelize_supported(int N);
 bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length
 int64_t front_hist_samples(int N);  // ADC history the fused kernel reads before a chunk

@@ -183,6 +183,29 @@ typedef struct mkid_replay_cfg {
 int mkid_replay_trigger(mkid_ctx* ctx, const int16_t* d_raw, int64_t n, int64_t ld, int32_t nch,
                         const mkid_replay_cfg* cfg, int32_t* d_hits, int32_t cap, int32_t* d_counts);
 
+/* Pulse template and near-optimal filter: MakeTemplate
+ * (DataReadout/ReadoutControls/lib/pulses.py:239-427) on device for one resonator's pulses, the
+ * reference's RawPulse rows I, Q float32 [npulses][2000] (pulses.py:30-43; not modified).
+ * Outputs the PulseAnalysis fields (pulses.py:44-51): template [2000] f64 (deg-normalised,
+ * peak at pstart), noise PSD [800] f64, and the scalars below. Fails with MKID_E_STATE when no
+ * pulse survives the first pass. */
+typedef struct mkid_template_info {
+    double count;   /* pulses in the final template (pass 2)                         */
+    double count1;  /* pulses in the preliminary template (pass 1, first 1000 pulses) */
+    double pm;      /* median of first-pass peaks > 15 deg (pulses.py:335)            */
+    double pdev;    /* their std                                                      */
+    int32_t flag;   /* 1 if count < 500 or pm < 10 or pm > 150 (pulses.py:409-412)    */
+    int32_t pstart; /* index of the template maximum (pulses.py:415)                  */
+} mkid_template_info;
+int mkid_make_template(mkid_ctx* ctx, const float* d_I, const float* d_Q, int64_t npulses,
+                       double* d_template, double* d_noise, mkid_template_info* info);
+/* The optimal filter the reference stubs (pulses.py:398; PulseAnalysis.coeff Float32Col(100)):
+ * correlation weights g = ifft(S / J) (S = fft of the 800-sample template window starting `pre`
+ * samples before its peak, deg->rad; J = noise PSD; DC bin zeroed), normalised to unit response
+ * to the template; d_coeff[0..ncoeff) = g[pre-10 ...]. Device in, device out. */
+int mkid_optimal_filter(mkid_ctx* ctx, const double* d_template, const double* d_noise, int32_t pre,
+                        int32_t ncoeff, double* d_coeff);
+
 /* Kernel timing with HIP events on the context stream (for bench roofline numbers). */
 #define MKID_K_CHANNELIZE 0
 #define MKID_K_FIR_PHASE 1

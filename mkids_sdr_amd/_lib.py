@@ -51,6 +51,11 @@ class ReplayCfg(ctypes.Structure):
                 ('threshold_deg', ctypes.c_double)]
 
 
+class TemplateInfo(ctypes.Structure):
+    _fields_ = [('count', ctypes.c_double), ('count1', ctypes.c_double), ('pm', ctypes.c_double),
+                ('pdev', ctypes.c_double), ('flag', ctypes.c_int32), ('pstart', ctypes.c_int32)]
+
+
 class SynthTone(ctypes.Structure):
     _fields_ = [('amp', ctypes.c_float), ('phase0', ctypes.c_float),
                 ('freq_index', ctypes.c_int32), ('pad', ctypes.c_int32)]
@@ -87,6 +92,8 @@ _SIGS = {
     'mkid_set_timing': [P, I32],
     'mkid_get_timing': [P, I32, P, P],
     'mkid_replay_trigger': [P, P, I64, I64, I32, P, P, I32, P],
+    'mkid_make_template': [P, P, P, I64, P, P, P],
+    'mkid_optimal_filter': [P, P, P, I32, I32, P],
     'mkid_synth_adc': [P, P, I64, I64, P, P, P, I64, ctypes.c_float, ctypes.c_float, I32,
                        ctypes.c_float, ctypes.c_uint32],
 }

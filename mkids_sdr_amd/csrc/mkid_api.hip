@@ -194,6 +194,20 @@ static void default_pfb(int N, int T, std::vector<float>& h) {
     for (int n = 0; n < L; ++n) h[n] = (float)(d[n] / s);
 }
 
+// scoped device allocations for the (non-hot-path) template calls
+struct DevBufs {
+    std::vector<void*> p;
+    ~DevBufs() { for (void* q : p) (void)hipFree(q); }
+    template <typename T>
+    hipError_t get(T** out, size_t n) {
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) p.push_back(q);
+        *out = (T*)q;
+        return e;
+    }
+};
+
 extern "C" {
 
 const char* mkid_global_error(void) { return g_err.c_str(); }
@@ -701,6 +715,66 @@ int mkid_replay_trigger(mkid_ctx* c, const int16_t* d_raw, int64_t n, int64_t ld
     HIPCHK(c, launch_replay(d_raw, n, ld, nch, rc->mode, rc->length, rc->start, rc->need, rc->skip,
                             rc->wrap_negative, rc->threshold_deg, c->d_rflags, c->d_rmeans, d_hits, cap,
                             d_counts, c->stream));
+    return MKID_OK;
+}
+
+int mkid_make_template(mkid_ctx* c, const float* d_I, const float* d_Q, int64_t P, double* d_template,
+                       double* d_noise, mkid_template_info* info) {
+    if (!c || !d_I || !d_Q || !d_template || !d_noise || !info) return MKID_E_ARG;
+    if (P <= 0) FAIL(c, MKID_E_ARG, "make_template: need pulses");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t N = 2000, NN = 800;
+    DevBufs b;
+    float *I, *Q, *refmed;
+    double *rows, *nrows, *peaks, *scratch, *tP, *stats;
+    int32_t *accept, *appended;
+    HIPCHK(c, b.get(&I, (size_t)P * N));
+    HIPCHK(c, b.get(&Q, (size_t)P * N));
+    HIPCHK(c, b.get(&rows, (size_t)P * N));
+    HIPCHK(c, b.get(&nrows, (size_t)P * NN));
+    HIPCHK(c, b.get(&peaks, (size_t)P));
+    HIPCHK(c, b.get(&scratch, (size_t)2 * P + 8));
+    HIPCHK(c, b.get(&tP, N));
+    HIPCHK(c, b.get(&stats, 8));
+    HIPCHK(c, b.get(&refmed, 2));
+    HIPCHK(c, b.get(&accept, (size_t)P));
+    HIPCHK(c, b.get(&appended, (size_t)P));
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(I, d_I, (size_t)P * N * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(Q, d_Q, (size_t)P * N * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemsetAsync(appended, 0, (size_t)P * 4, s));
+    HIPCHK(c, hipMemsetAsync(stats, 0, 64, s));
+    hipError_t e = launch_make_template(I, Q, P, rows, nrows, accept, peaks, appended, scratch, tP, d_template,
+                                        d_noise, stats, refmed, s);
+    if (e == hipErrorInvalidValue) FAIL(c, MKID_E_STATE, "make_template: no pulse passed the first pass");
+    HIPCHK(c, e);
+    double st[5];
+    std::vector<double> t(N);
+    HIPCHK(c, hipMemcpyAsync(st, stats, 40, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(t.data(), d_template, N * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    info->pm = st[0];
+    info->pdev = st[1];
+    info->count1 = st[3];
+    info->count = st[4];
+    info->flag = (st[4] < 500 || st[0] < 10 || st[0] > 150) ? 1 : 0;
+    int ps = 0;
+    for (size_t i = 1; i < N; ++i)
+        if (t[i] > t[ps]) ps = (int)i;
+    info->pstart = ps;
+    return MKID_OK;
+}
+
+int mkid_optimal_filter(mkid_ctx* c, const double* d_template, const double* d_noise, int32_t pre, int32_t ncoeff,
+                        double* d_coeff) {
+    if (!c || !d_template || !d_noise || !d_coeff) return MKID_E_ARG;
+    if (pre < 10 || pre > 2000 || ncoeff <= 0 || ncoeff > 800) FAIL(c, MKID_E_ARG, "optimal_filter: bad pre/ncoeff");
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBufs b;
+    double* work;
+    HIPCHK(c, b.get(&work, 3 * 800));
+    HIPCHK(c, launch_optimal_filter(d_template, d_noise, pre, ncoeff, d_coeff, work, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return MKID_OK;
 }
 

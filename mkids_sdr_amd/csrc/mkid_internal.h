@@ -111,6 +111,12 @@ hipError_t launch_replay(const int16_t* raw, int64_t n, int64_t ld, int32_t nch,
                          int64_t start, int64_t need, int64_t skip, int32_t wrap, double thr, uint32_t* flags,
                          double* means, int32_t* hits, int32_t cap, int32_t* counts, hipStream_t s);
 
+hipError_t launch_make_template(float* I, float* Q, int64_t P, double* rows, double* nrows, int32_t* accept,
+                                double* peaks, int32_t* appended, double* scratch, double* tP, double* tPf,
+                                double* noise, double* stats, float* refmed, hipStream_t s);
+hipError_t launch_optimal_filter(const double* tpl, const double* noise, int pre, int ncoeff, double* coeff,
+                                 double* work, hipStream_t s);
+
 bool channelize_supported(int N);
 bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length
 int64_t front_hist_samples(int N);  // ADC history the fused kernel reads before a chunk

@@ -146,6 +146,13 @@ int mkid_last_raw_phase(mkid_ctx* ctx, const int16_t** d_raw, int64_t* nrows);
  * snapshot readback (conv_phase_snapPhase_bram / qdr0 longsnapshot, ROACH_Pulses.py:433-551). */
 int mkid_read_raw_phase(mkid_ctx* ctx, int16_t* host_out, int64_t cap_rows, int64_t* rows);
 
+/* IQ snapshot tap (conv_phase_ch_we_IQ / conv_phase_snapIQ_bram, pulse_triggering_IQ.py:36,
+ * 113-147): record the low-pass output y of one channel (channel < 0: off) for the rows of each
+ * process call, as int16 I/Q pairs in ADC-count units (the units of mkid_avg_iq and the IQ
+ * centres; saturated). mkid_read_iq_tap copies the last call's rows [rows][2] to the host. */
+int mkid_set_iq_tap(mkid_ctx* ctx, int32_t channel);
+int mkid_read_iq_tap(mkid_ctx* ctx, int16_t* host_iq, int64_t cap_rows, int64_t* rows);
+
 /* Diagnostic: trigger segments of the last sub-chunk whose speculative start state had to be
  * re-run by the exact fix-up pass (0 = all speculation was right; results are exact either way). */
 int mkid_trigger_reruns(mkid_ctx* ctx, int64_t* total);

@@ -86,6 +86,8 @@ _SIGS = {
     'mkid_process_device': [P, P, I64, P, P, I64, P],
     'mkid_last_raw_phase': [P, P, P],
     'mkid_read_raw_phase': [P, P, I64, P],
+    'mkid_set_iq_tap': [P, I32],
+    'mkid_read_iq_tap': [P, P, I64, P],
     'mkid_avg_iq': [P, P, P],
     'mkid_trigger_reruns': [P, P],
     'mkid_pack_reference': [P, I64, P],

@@ -138,6 +138,18 @@ class Channelizer:
         self._chk(self._L.mkid_read_raw_phase(self._h, _ptr(out), rows, ctypes.byref(n)))
         return out
 
+    def set_iq_tap(self, channel):
+        """Record channel's low-pass output (IQ snapshot source); channel < 0 turns it off."""
+        self._chk(self._L.mkid_set_iq_tap(self._h, int(channel)))
+
+    def iq_tap(self):
+        """int16 [rows][2] I/Q of the tapped channel for the rows of the last process call."""
+        n = ctypes.c_int64()
+        self._chk(self._L.mkid_read_iq_tap(self._h, None, 0, ctypes.byref(n)))
+        out = np.empty((n.value, 2), np.int16)
+        self._chk(self._L.mkid_read_iq_tap(self._h, _ptr(out), n.value, ctypes.byref(n)))
+        return out
+
     def trigger_reruns(self):
         n = ctypes.c_int64()
         self._chk(self._L.mkid_trigger_reruns(self._h, ctypes.byref(n)))

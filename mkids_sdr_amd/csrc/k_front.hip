@@ -277,6 +277,10 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
                     if (phase_run) phase_run[jr * C + c] = ph;
 #endif
                     raw_run[jr * C + c] = (int16_t)q;
+                    if (c == a.iq_ch && a.iqtap) {  // IQ snapshot tap (conv_phase_snapIQ_bram)
+                        a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y.x);
+                        a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y.y);
+                    }
                 }
             }
         }

@@ -58,6 +58,10 @@ __global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
                 q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
                 if (a.phase) a.phase[j * C + c] = ph;
                 a.raw[j * C + c] = (int16_t)q;
+                if (c == a.iq_ch && a.iqtap) {
+                    a.iqtap[2 * j] = iq16(yr);
+                    a.iqtap[2 * j + 1] = iq16(yi);
+                }
             }
         }
     }

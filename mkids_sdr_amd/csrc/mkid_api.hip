@@ -83,6 +83,10 @@ struct mkid_ctx {
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
     int64_t last_J = 0;     // phase rows of the last call
     int64_t last_subJ = 0;  // rows of its last sub-chunk (held in d_raw)
+    // IQ snapshot tap: low-pass output of one channel for the rows of the last call
+    int32_t iq_ch = -1;
+    int16_t* d_iqtap = nullptr;     // [max_chunk/N][2]
+    int64_t iq_rows = 0;
     // replay-trigger workspace (lazy, grown on demand)
     uint32_t* d_rflags = nullptr;
     double* d_rmeans = nullptr;
@@ -160,7 +164,7 @@ static void free_all(mkid_ctx* c) {
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
-                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans};
+                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -302,6 +306,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
         AL(d_zb[1], (size_t)c->Kmax * C);
     }
     AL(d_raw, (size_t)c->Jmax * C);
+    AL(d_iqtap, (size_t)(cfg->max_chunk / N) * 2);
     AL(d_ysum, C);
     AL(d_slots, (size_t)c->slot_cap);
     AL(d_chcounts, (size_t)C * c->nseg_max);
@@ -512,6 +517,8 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.avail = off;
         fa.P = c->P;
         fa.taps = c->lpf;
+        fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
+        fa.iq_ch = c->iq_ch;
         tstart(c, MKID_K_FRONT, &kt, s);
         HIPCHK(c, launch_front(N, fa, s));
         tstop(c, &kt, s);
@@ -524,6 +531,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     }
     HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, c->H, n, 4, s));
     HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)c->H * 4, hipMemcpyDeviceToDevice, s));
+    c->iq_rows = c->iq_ch >= 0 ? n / N : 0;
     return MKID_OK;
 }
 
@@ -562,7 +570,8 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
         // ---- stream B: low-pass + phase, trigger, compaction of this sub-chunk ----
         HIPCHK(c, hipStreamWaitEvent(B, c->ev_zready[b], 0));
         LpfArgs la{z, zprev, c->d_ic, c->d_qc, d_phase ? d_phase + (off / N) * C : nullptr,
-                   c->d_raw, c->d_ysum, J, C, c->lpf};
+                   c->d_raw, c->d_ysum, J, C, c->lpf,
+                   c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr, c->iq_ch};
         tstart(c, MKID_K_FIR_PHASE, &kt, B);
         HIPCHK(c, launch_lpf_phase(la, B));
         tstop(c, &kt, B);
@@ -595,6 +604,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     // ... and A (the caller's stream) waits for everything B did
     HIPCHK(c, hipEventRecord(c->ev_done, B));
     HIPCHK(c, hipStreamWaitEvent(A, c->ev_done, 0));
+    c->iq_rows = c->iq_ch >= 0 ? n / N : 0;
     return MKID_OK;
 }
 
@@ -654,6 +664,25 @@ int mkid_read_raw_phase(mkid_ctx* c, int16_t* host_out, int64_t cap_rows, int64_
     if (n <= 0) return MKID_OK;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(host_out, c->d_raw, (size_t)n * c->C * 2, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MKID_OK;
+}
+
+int mkid_set_iq_tap(mkid_ctx* c, int32_t channel) {
+    if (!c) return MKID_E_ARG;
+    if (channel >= c->C) FAIL(c, MKID_E_ARG, "iq tap channel out of range");
+    c->iq_ch = channel < 0 ? -1 : channel;
+    c->iq_rows = 0;
+    return MKID_OK;
+}
+
+int mkid_read_iq_tap(mkid_ctx* c, int16_t* host_iq, int64_t cap_rows, int64_t* rows) {
+    if (!c || !rows || (cap_rows > 0 && !host_iq)) return MKID_E_ARG;
+    *rows = c->iq_rows;
+    const int64_t n = std::min(c->iq_rows, cap_rows);
+    if (n <= 0) return MKID_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(host_iq, c->d_iqtap, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return MKID_OK;
 }

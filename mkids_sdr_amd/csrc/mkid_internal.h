@@ -24,6 +24,12 @@ static_assert(sizeof(TrigState) == 48, "TrigState layout");
 
 struct LpfTaps { float g[kFirTaps]; };
 
+// IQ snapshot sample: the low-pass output in ADC-count units, rounded and saturated to int16
+__device__ __forceinline__ int16_t iq16(float v) {
+    const float r = rintf(v);
+    return (int16_t)(r < -32768.f ? -32768.f : (r > 32767.f ? 32767.f : r));
+}
+
 struct ChanArgs {
     const uint32_t* x;      // chunk, int16 I/Q packed per 32-bit word
     const uint32_t* xhist;  // T*N - M previous samples
@@ -51,6 +57,8 @@ struct LpfArgs {
     int64_t J;
     int32_t C;
     LpfTaps taps;
+    int16_t* iqtap;         // [J][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
+    int32_t iq_ch;
 };
 
 struct FrontArgs {
@@ -71,6 +79,8 @@ struct FrontArgs {
     int32_t P;              // LO period (power of two)
     int32_t pad;
     LpfTaps taps;
+    int16_t* iqtap;         // [K/2][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
+    int32_t iq_ch;
 };
 
 struct TrigSpecArgs {

@@ -16,7 +16,11 @@ Register map:
            capture_Baseline_alpha, capture_base_Kf, capture_base_Kq, capture_base_thresh
   control  startDAC, DRAM_LUT_rd_valid, startAccumulator, avgIQ_ctrl, startSnap, snapPhase_ctrl,
            ch_we, startBuffer
-  readback avgIQ_bram, snapPhase_bram, pulses_addr, pulses_bram0/1
+  readback avgIQ_bram, snapPhase_bram (ROACH_Pulses.py snapshot, swapped halves), qdr0_memory
+           (longsnapshot, ROACH_Pulses.py:433-551), conv_phase_snapPhase_bram /
+           conv_phase_snapIQ_bram with conv_phase_ch_we_Phase / conv_phase_ch_we_IQ
+           (pulse_triggering_v2.py:36-95, pulse_triggering_IQ.py:36-147), pulses_addr,
+           pulses_bram0/1
 Errors are raised as RuntimeError (katcp semantics, pulse_triggering_v2.py:177-179).
 """
 import re
@@ -120,8 +124,11 @@ class FpgaClient:
             self.cfg.dirty.add('baseline')
         elif name == 'startBuffer':
             self._buffering = bool(value)
+        elif name == 'conv_phase_ch_we_IQ' and self._chan is not None:
+            self._chan.set_iq_tap(value)
         elif name in ('startAccumulator', 'startSnap', 'startDAC', 'avgIQ_ctrl', 'snapPhase_ctrl',
-                      'snapqdr_ctrl', 'ch_we'):
+                      'snapqdr_ctrl', 'ch_we', 'conv_phase_ch_we_Phase', 'conv_phase_startSnapIQ',
+                      'conv_phase_startSnapPhase', 'conv_phase_snapIQ_ctrl', 'conv_phase_snapPhase_ctrl'):
             pass  # control strobes: state is read back through self.regs
         return None
 
@@ -159,6 +166,16 @@ class FpgaClient:
             return self._read_avgiq(size)
         if name == 'snapPhase_bram':
             return self._read_snap_phase(size)
+        if name == 'qdr0_memory':
+            # longsnapshot: 2 Fix16_13 samples per 32-bit word, '>h' in time order
+            raw = self._raw_of(self.regs.get('ch_we', 0), size // 2)
+            return raw.astype('>i2').tobytes()[:size]
+        if name == 'conv_phase_snapPhase_bram':
+            raw = self._raw_of(self.regs.get('conv_phase_ch_we_Phase', 0), size // 4)
+            return codecs.encode_conv_phase_snap(raw)[:size]
+        if name == 'conv_phase_snapIQ_bram':
+            I, Q = self._iq_of(self.regs.get('conv_phase_ch_we_IQ', 0), size // 8)
+            return codecs.encode_iq_snap(I, Q)[:size]
         if name in ('pulses_bram0', 'pulses_bram1'):
             w0, w1 = codecs.reference_bram_words(self._ring)
             w = w0 if name == 'pulses_bram0' else w1
@@ -218,6 +235,27 @@ class FpgaClient:
         mi, mq = ch.avg_iq()
         words = np.concatenate([np.rint(mi), np.rint(mq)]).astype('>i4')
         return words.tobytes()[:size]
+
+    def _raw_of(self, ch, nsamp):
+        """Fix16_13 phase of channel ch for the next nsamp phase samples (device raw values:
+        rint(phase * 8192) of the float32 phase, clamped, exactly as k_front quantises)."""
+        phase, _ = self.run(nsamp)
+        return np.clip(np.rint(phase[:, ch] * np.float32(8192)), -25736, 25736).astype(np.int64)
+
+    def _iq_of(self, ch, npairs):
+        """Low-pass I/Q of channel ch for the next npairs phase samples (device IQ tap)."""
+        c = self.sync()
+        c.set_iq_tap(ch)
+        step = max(1, int(c.cfg.max_chunk) // self.N)
+        out = []
+        left = npairs
+        while left > 0:
+            n = min(step, left)
+            c.process(self.adc(n * self.N))
+            out.append(c.iq_tap())
+            left -= n
+        iq = np.concatenate(out).astype(np.int64) if out else np.zeros((0, 2), np.int64)
+        return iq[:, 0], iq[:, 1]
 
     def _read_snap_phase(self, size):
         nsamp = size // 2

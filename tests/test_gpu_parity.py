@@ -229,3 +229,30 @@ def test_errors_are_loud(gpu):
         ch.close()
     with pytest.raises(_lib.MkidError):
         Channelizer(100)                                      # N = 200 unsupported
+
+
+@pytest.mark.parametrize('front', ['auto', 'split'])
+def test_iq_snapshot_tap_matches_oracle(gpu, front):
+    """mkid_set_iq_tap: the tapped channel's low-pass output equals the oracle's y, rounded."""
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 256, 2 ** 17
+    case = signals.make_case(C, S, seed=41, pulses_per_ch=1.0)
+    y = signals.oracle_chain(case).process(case.iq)['y']
+    ch = Channelizer(C, max_chunk=S, front=front)
+    try:
+        configure(ch, case, np.full(C, -(1 << 30), np.int64))
+        tone = int(np.argmax(np.abs(y).mean(0)))
+        ch.set_iq_tap(tone)
+        ch.process(case.iq)
+        iq = ch.iq_tap().astype(np.int64)
+        exp = np.stack([np.rint(y[:, tone].real), np.rint(y[:, tone].imag)], 1)
+        exp = np.clip(exp, -32768, 32767).astype(np.int64)
+        assert iq.shape == exp.shape
+        d = np.abs(iq - exp)
+        assert d.max() <= 1 and (d > 0).mean() < 1e-3
+        assert np.abs(exp).max() > 100                      # a live tone, not zeros
+        ch.set_iq_tap(-1)
+        ch.process(case.iq[:2 * C * 8])
+        assert ch.iq_tap().shape == (0, 2)
+    finally:
+        ch.close()

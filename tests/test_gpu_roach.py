@@ -42,3 +42,52 @@ def test_setup_rotate_threshold_flow(gpu):
     assert len(snap) == 2 * 2 * 1024 and np.abs(snap).max() < 2000   # near 0 after rotation
     pulses = rp.readPulses(steps=2)
     assert sum(len(v) for v in pulses.values()) < 50   # noise only: few or no triggers
+
+
+def _ref_iq_decode(buf):
+    """pulse_triggering_IQ.py:121-147 verbatim in spirit: hex strings per byte, nibble slicing."""
+    def twos_comp(val, bits):
+        if (val & (1 << (bits - 1))) != 0:
+            val = val - (1 << bits)
+        return val
+    hx = ["0x{:02x}".format(b) for b in buf]
+    I, Q = [], []
+    for k in range(len(buf) // 16):
+        I.append(twos_comp(int(hx[6 + 16 * k][3] + hx[7 + 16 * k][2:4] + hx[8 + 16 * k][2], 16), 16))
+        I.append(twos_comp(int(hx[11 + 16 * k][3] + hx[12 + 16 * k][2:4] + hx[13 + 16 * k][2], 16), 16))
+        Q.append(twos_comp(int(hx[9 + 16 * k][2:4] + hx[10 + 16 * k][2:4], 16), 16))
+        Q.append(twos_comp(int(hx[14 + 16 * k][2:4] + hx[15 + 16 * k][2:4], 16), 16))
+    return np.array(I), np.array(Q)
+
+
+def test_snapshot_registers_readback(gpu):
+    """conv_phase_snapIQ_bram / conv_phase_snapPhase_bram / qdr0_memory served from the GPU and
+    decoded the way the reference scripts decode them."""
+    import struct
+    C = 256
+    roach = FpgaClient(n_channels=C, noise_sigma=20.0, seed=5)
+    roach.progdev('pulse_trigger_2022_Jan_24_1322.bof')
+    freqs = list(4.0e9 + np.array([-120, -40, 30, 95]) * 1e6 + 15625.0)
+    rs = RoachSetup(roach, freqs, 4.0e9, n_channels=C)
+    rs.define_LUTs()
+    rs.toggleDAC()
+    rs.read_avg_iq()
+    rs.rotateLoopsReady()
+    rs.loadIQcenters()
+    ch = 1
+    roach.write_int('conv_phase_ch_we_IQ', ch)
+    L_IQ = 1024
+    I, Q = _ref_iq_decode(roach.read('conv_phase_snapIQ_bram', 4 * L_IQ))
+    assert len(I) == L_IQ // 2
+    Ic, Qc = roach.cfg.ic[ch], roach.cfg.qc[ch]
+    ph = -360 * np.arctan2(Q - Qc, I - Ic) / (2 * np.pi)     # pulse_triggering_IQ.py:152
+    assert np.abs(np.hypot(I - Ic, Q - Qc)).mean() > 50       # on the loop, not at its centre
+    assert np.abs(np.median(ph)) < 5.0                        # rotated loop: phase ~ 0
+    roach.write_int('conv_phase_ch_we_Phase', ch)
+    buf = roach.read('conv_phase_snapPhase_bram', 4 * 512)
+    raw = [struct.unpack('>h', buf[4 * m + 2:4 * m + 4])[0] for m in range(512)]  # v2.py:93
+    assert np.abs(np.median(raw)) < 1000
+    roach.write_int('ch_we', ch)
+    q = roach.read('qdr0_memory', 4 * 1024)
+    vals = struct.unpack('>%dh' % 2048, q)                     # ROACH_Pulses.py:471
+    assert len(vals) == 2048 and np.abs(np.median(vals)) < 1000

@@ -109,13 +109,17 @@ __global__ __launch_bounds__(kSpecThreads) void k_trig_spec(TrigSpecArgs a) {
     const int64_t sc = (int64_t)c * a.nseg + s;
     uint64_t* slot = a.slots + sc * a.capseg;
     int32_t n = 0;
-    const int16_t* rp = a.raw + jw * C + c;  // running pointer: no 64-bit index multiplies
+    // all lanes of a wave share the segment (64 | C): a scalar row base and a 32-bit per-lane
+    // offset give SGPR-base loads (no 64-bit address arithmetic per sample)
+    const char* rbase = reinterpret_cast<const char*>(a.raw + (int64_t)__builtin_amdgcn_readfirstlane((int32_t)jw) * C);
+    uint32_t roff = (uint32_t)c * 2u;  // byte offset (a 32-bit VGPR next to an SGPR base)
+    auto rload = [&](uint32_t off) { return (int32_t)*reinterpret_cast<const int16_t*>(rbase + off); };
     // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0
     for (int32_t gi = 0; gi < (int32_t)(seg0 - jw); gi += kFirTaps) {
         int32_t r[kFirTaps];
 #pragma unroll
-        for (int u = 0; u < kFirTaps; ++u) r[u] = rp[(int64_t)u * C];  // all loads in flight
-        rp += (int64_t)kFirTaps * C;
+        for (int u = 0; u < kFirTaps; ++u) r[u] = rload(roff + (uint32_t)(2 * u * C));  // all loads in flight
+        roff += (uint32_t)(2 * kFirTaps * C);
 #pragma unroll
         for (int u = 0; u < kFirTaps; ++u) {
             EvInfo ev;
@@ -129,8 +133,8 @@ __global__ __launch_bounds__(kSpecThreads) void k_trig_spec(TrigSpecArgs a) {
     for (; gi < full; gi += kFirTaps) {
         int32_t r[kFirTaps];
 #pragma unroll
-        for (int u = 0; u < kFirTaps; ++u) r[u] = rp[(int64_t)u * C];
-        rp += (int64_t)kFirTaps * C;
+        for (int u = 0; u < kFirTaps; ++u) r[u] = rload(roff + (uint32_t)(2 * u * C));
+        roff += (uint32_t)(2 * kFirTaps * C);
 #pragma unroll
         for (int u = 0; u < kFirTaps; ++u) {
             const int32_t f = mf_q(win, tp, u, r[u]);
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(kSpecThreads) void k_trig_spec(TrigSpecArgs a) {
 #pragma unroll
     for (int u = 0; u < kFirTaps; ++u) {
         if (u < left) {
-            const int32_t f = mf_q(win, tp, u, rp[(int64_t)u * C]);
+            const int32_t f = mf_q(win, tp, u, rload(roff + (uint32_t)(2 * u * C)));
             EvInfo ev;
             if (trig_update(st, f, k, ev)) {
                 if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);

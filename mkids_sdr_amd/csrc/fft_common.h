@@ -225,6 +225,33 @@ struct TwiddleRec {
     }
 };
 
+// Twiddles of one pass read from an LDS table (entry m = j mod NS holds w^1..w^(R-1),
+// w = exp(-2 pi i m / (NS R)), 8 B each, stride (R-1) float2: conflict-free ds_read_b64 for
+// consecutive m, broadcast for NS < 64) instead of being rebuilt by complex multiplies.
+template <int N, int PTS, int R, int NS>
+struct TwiddleLds {
+    static constexpr int NB = PTS / R;
+    static constexpr int ENTRIES = NS * (R - 1);  // float2 in the table
+    const float2* tab;
+    __device__ __forceinline__ static void fill(float2* tab, int tid, int nthreads) {
+        for (int i = tid; i < ENTRIES; i += nthreads) {
+            const int m = i / (R - 1), r = i % (R - 1) + 1;
+            double sn, cs;
+            sincospi(-2.0 * (double)(m * r) / (double)(NS * R), &sn, &cs);
+            tab[i] = make_float2((float)cs, (float)sn);
+        }
+    }
+    __device__ __forceinline__ void apply(float2 (&v)[PTS], int t) const {
+        constexpr int NT = N / PTS;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const float2* e = tab + ((t + q * NT) % NS) * (R - 1);
+#pragma unroll
+            for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], e[r - 1]);
+        }
+    }
+};
+
 template <int N>
 struct Plan8;  // PTS = 8 points per thread; radix sequence R1..R4 (1 = no pass)
 template <> struct Plan8<128>  { static constexpr int NP = 3, R[4] = {8, 4, 4, 1}; };

@@ -77,7 +77,10 @@ struct FGeo {
     static constexpr int RL = FPlan<N>::R[FPlan<N>::NP - 1];  // radix of the fused last pass
     static constexpr int NSL = N / RL;                        // its butterfly count / stride
     static_assert(NSL % 16 == 0, "pad-linear offsets in the fused last pass");
-    static constexpr size_t lds_bytes = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8 + (size_t)N * 16;
+    using TW2 = TwiddleLds<N, PTS, FPlan<N>::R[1], NS2>;
+    using TW3 = TwiddleLds<N, PTS, (FPlan<N>::NP == 4 ? FPlan<N>::R[2] : 2), NS3>;
+    static constexpr size_t tw_offset = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8 + (size_t)N * 16;
+    static constexpr size_t lds_bytes = tw_offset + (size_t)(TW2::ENTRIES + TW3::ENTRIES) * 8;
     static constexpr int HIST = (2 * T - 1 + kLpfHist) * M;  // ADC history samples
     // register budget sized for 4 waves per SIMD (16 per CU, <= 128 VGPRs): HIP's second
     // launch-bounds argument is the minimum waves per execution unit
@@ -114,10 +117,12 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     for (int p = tid; p < N; p += G::BT)
         hl[p] = make_float4(a.pfb[p], a.pfb[N + p], a.pfb[2 * N + p], a.pfb[3 * N + p]);
 
-    TwiddleRec<N, PTS, PL::R[1], G::NS2> tw2;
-    tw2.init(t);
-    TwiddleRec<N, PTS, (PL::NP == 4 ? PL::R[2] : 2), G::NS3> tw3;
-    if constexpr (PL::NP == 4) tw3.init(t);
+    // pass-2/3 twiddle tables in LDS (filled once; published by the prologue barrier)
+    float2* twt = reinterpret_cast<float2*>(smem + G::tw_offset);
+    typename G::TW2 tw2{twt};
+    typename G::TW3 tw3{twt + G::TW2::ENTRIES};
+    G::TW2::fill(twt, tid, G::BT);
+    if constexpr (PL::NP == 4) G::TW3::fill(twt + G::TW2::ENTRIES, tid, G::BT);
 
     const int c = tid;  // channel of the select / low-pass / phase stage
     const int32_t bin = a.bins[c];
@@ -213,14 +218,14 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         FSYNC(1);
         st_read<N, PTS, PL::R[1]>(buf, v, t);
         FSYNC(2);
-        tw2.apply(v);
+        tw2.apply(v, t);
         st_dft<PTS, PL::R[1]>(v);
         if constexpr (PL::NP == 4) {
             st_write<N, PTS, PL::R[1], G::NS2, typename G::PadB>(buf, v, t);
             FSYNC(3);
             st_read<N, PTS, PL::R[2], typename G::PadB>(buf, v, t);
             FSYNC(4);
-            tw3.apply(v);
+            tw3.apply(v, t);
             st_dft<PTS, PL::R[2]>(v);
             st_write<N, PTS, PL::R[2], G::NS3>(buf, v, t);
             FSYNC(5);

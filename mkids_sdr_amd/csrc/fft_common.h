@@ -1,4 +1,4 @@
-// Radix-2/4/8/16 forward DFT butterflies and Stockham LDS passes for the channeliser FFT.
+// Radix-2/4/8 forward DFT butterflies and Stockham LDS passes for the channeliser FFT.
 // Sign convention: X[k] = sum_n x[n] exp(-2 pi i n k / N) (numpy.fft.fft).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -50,35 +50,6 @@ __device__ __forceinline__ void dft<8>(float2* v) {
     v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
     v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
     v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
-}
-
-template <>
-__device__ __forceinline__ void dft<16>(float2* v) {
-    // n = r + 4m, k = s + 4q: X[s+4q] = sum_r W4^{rq} W16^{rs} sum_m x[r+4m] W4^{ms}
-    constexpr float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
-    constexpr float r2 = 0.70710678118654752440f;
-    float2 b[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        b[r][0] = v[r]; b[r][1] = v[r + 4]; b[r][2] = v[r + 8]; b[r][3] = v[r + 12];
-        dft4(b[r][0], b[r][1], b[r][2], b[r][3]);
-    }
-    const float2 w1 = make_float2(c1, -s1), w2 = make_float2(r2, -r2), w3 = make_float2(s1, -c1);
-    b[1][1] = cmul(b[1][1], w1);
-    b[1][2] = cmul(b[1][2], w2);
-    b[1][3] = cmul(b[1][3], w3);
-    b[2][1] = cmul(b[2][1], w2);
-    b[2][2] = mul_mi(b[2][2]);
-    b[2][3] = cmul(b[2][3], make_float2(-r2, -r2));
-    b[3][1] = cmul(b[3][1], w3);
-    b[3][2] = cmul(b[3][2], make_float2(-r2, -r2));
-    b[3][3] = cmul(b[3][3], make_float2(-c1, s1));  // W16^9 = -W16^1
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        float2 a0 = b[0][s], a1 = b[1][s], a2 = b[2][s], a3 = b[3][s];
-        dft4(a0, a1, a2, a3);
-        v[s] = a0; v[s + 4] = a1; v[s + 8] = a2; v[s + 12] = a3;
-    }
 }
 
 // LDS index padding: one float2 of pad every 16 entries (breaks power-of-two lane strides).
@@ -151,32 +122,6 @@ __device__ __forceinline__ void st_dft(float2 (&v)[PTS]) {
 #pragma unroll
     for (int q = 0; q < PTS / R; ++q) dft<R>(&v[q * R]);
 }
-
-// Twiddles of one pass for this thread's butterflies: w[q][r-1] = exp(-2 pi i (j%NS) r / (NS R)).
-template <int N, int PTS, int R, int NS>
-struct Twiddle {
-    static constexpr int NB = PTS / R;
-    float2 w[NB * (R - 1) > 0 ? NB * (R - 1) : 1];
-    __device__ __forceinline__ void init(int t) {
-        constexpr int NT = N / PTS;
-#pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            const int m = (t + q * NT) % NS;
-#pragma unroll
-            for (int r = 1; r < R; ++r) {
-                double s, c;
-                sincospi(-2.0 * (double)(m * r) / (double)(NS * R), &s, &c);
-                w[q * (R - 1) + r - 1] = make_float2((float)c, (float)s);
-            }
-        }
-    }
-    __device__ __forceinline__ void apply(float2 (&v)[PTS]) const {
-#pragma unroll
-        for (int q = 0; q < NB; ++q)
-#pragma unroll
-            for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], w[q * (R - 1) + r - 1]);
-    }
-};
 
 // Register-lean twiddles: one base w = exp(-2 pi i (j%NS) / (NS R)) per butterfly; the powers
 // w^2..w^(R-1) are rebuilt by at most 6 complex multiplies per radix-8 butterfly (error a few ulp,

@@ -31,8 +31,14 @@ struct KTime {
 // Speculative trigger segmentation (k_trigger.hip): segments of kSegL phase samples, each
 // speculating from kSegW samples of warm-up. The EMA baseline (alpha 41/512) forgets its start
 // in ~10^2 samples on noisy phase; SVF runs as a single exact segment.
-constexpr int64_t kSegL = 2048;
-constexpr int64_t kSegW = 520;  // multiple of the 26-sample matched-filter ring
+#ifndef MKID_SEG_L
+#define MKID_SEG_L 2048
+#endif
+#ifndef MKID_SEG_W
+#define MKID_SEG_W 520
+#endif
+constexpr int64_t kSegL = MKID_SEG_L;
+constexpr int64_t kSegW = MKID_SEG_W;  // multiple of the 26-sample matched-filter ring
 static_assert(kSegW % kFirTaps == 0 && kSegL >= kSegW + kRawHist, "segment geometry");
 int64_t seg_capacity(int dead) { return kSegL / (dead + 3) + 2; }
 

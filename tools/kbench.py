@@ -86,6 +86,7 @@ def main():
             t = ch.timing()
             ch.set_timing(False)
             if r == 0:
+                times[path].setdefault('reruns', []).append(float(ch.trigger_reruns()))
                 continue  # warm-up round
             for k, (ms, n) in t.items():
                 times[path].setdefault(k, []).append(ms)

@@ -191,13 +191,11 @@ __global__ __launch_bounds__(Geo<N>::BT, MKID_CHAN_MINWAVES) void k_channelize(C
         // ---- bin select + DDC ----
         if (k < k_end) {
             const int64_t kg = a.k0 + k;
-            const int podd = (int)((kg + 1) & 1);
             const int lidx = (int)(kg & (a.P - 1));
 #pragma unroll
             for (int q = 0; q < G::CPT; ++q) {
                 const int c = t + q * NT;
                 float2 X = fin[lpad(bin[q])];
-                if (podd & bin[q] & 1) X = make_float2(-X.x, -X.y);
                 const float2 lo = a.lo[lidx * C + c];
                 a.z[k * C + c] = cmul(X, lo);
             }

@@ -12,7 +12,8 @@
 //          last pass is fused into the select: thread c evaluates only the radix-4 butterfly
 //          output X[bin_c] (4 LDS reads, 3 complex MACs with per-channel constant twiddles).
 //   DDC    thread c = channel c: z_k = X_k[bin_c] (-1)^(bin_c (k+1)) conj(LUT_c[k mod P]) / 2^15
-//          for the 4 frames of the iteration (LO table [P][C]: one contiguous row per frame).
+//          for the 4 frames of the iteration (LO table [P][C]: one contiguous row per frame; the
+//          bin-parity sign is folded into the table on the host, P being even).
 //   LPF    transposed form, 13 complex accumulators per thread: frame 2j adds g_{2m+1} z to
 //          output j+m, frame 2j+1 adds g_{2m} z and completes output j:
 //          y_j = sum_i g_i z_{2j+1-i}      (taps int(lpf*(2**11-1))/2^11, ROACH_Pulses.py:69,88)
@@ -127,7 +128,6 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     const int c = tid;  // channel of the select / low-pass / phase stage
     const int32_t bin = a.bins[c];
     const float ic = a.ic[c], qc = a.qc[c];
-    const int podd_mask = bin & 1;
     // fused last pass for X[bin]: bin = jl + NSL s,
     //   X[bin] = sum_r W_RL^{r s} W_N^{jl r} Y[jl + r NSL]   (Stockham last pass, NS = NSL)
     constexpr int RL = G::RL, NSL = G::NSL;
@@ -246,7 +246,6 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
                 X.x = fmaf(tl[r - 1].x, yv.x, fmaf(-tl[r - 1].y, yv.y, X.x));
                 X.y = fmaf(tl[r - 1].x, yv.y, fmaf(tl[r - 1].y, yv.x, X.y));
             }
-            if ((int)((a.k0 + k + 1) & 1) & podd_mask) X = make_float2(-X.x, -X.y);
             const float2 z = cmul(X, lov[f]);
 #ifdef MKID_XP_STAMPS
             if (f == 0) {

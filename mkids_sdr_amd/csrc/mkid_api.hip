@@ -93,6 +93,10 @@ struct mkid_ctx {
     int32_t iq_ch = -1;
     int16_t* d_iqtap = nullptr;     // [max_chunk/N][2]
     int64_t iq_rows = 0;
+    // host copies behind the folded LO table (d_lo = conj(LUT)/2^15 with the (-1)^(b (k+1))
+    // bin-parity sign of K4 folded in: P is even, so the sign depends on k mod P only)
+    std::vector<float2> h_lo;      // [P][C]
+    std::vector<int32_t> h_bins;   // [C]
     // replay-trigger workspace (lazy, grown on demand)
     uint32_t* d_rflags = nullptr;
     double* d_rmeans = nullptr;
@@ -218,6 +222,8 @@ struct DevBufs {
     }
 };
 
+static int upload_lo_folded(mkid_ctx* c);
+
 extern "C" {
 
 const char* mkid_global_error(void) { return g_err.c_str(); }
@@ -244,7 +250,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     if (N != 2 * C || !channelize_supported(N)) { g_err = "unsupported geometry: need N = 2C, N in {128..4096}"; return MKID_E_ARG; }
     if (cfg->pfb_taps != kPfbTaps || cfg->fir_taps != kFirTaps) { g_err = "pfb_taps must be 4 and fir_taps 26"; return MKID_E_ARG; }
     const int P = cfg->dds_entries;
-    if (P <= 0 || (P & (P - 1)) != 0) { g_err = "dds_entries must be a power of two"; return MKID_E_ARG; }
+    if (P < 2 || (P & (P - 1)) != 0) { g_err = "dds_entries must be a power of two >= 2"; return MKID_E_ARG; }
     if (cfg->max_chunk < N || cfg->max_chunk % N != 0) { g_err = "max_chunk must be a positive multiple of N"; return MKID_E_ARG; }
     if (cfg->dead_time < 0) { g_err = "dead_time < 0"; return MKID_E_ARG; }
     if (cfg->front != MKID_FRONT_AUTO && cfg->front != MKID_FRONT_SPLIT) { g_err = "bad front mode"; return MKID_E_ARG; }
@@ -341,8 +347,10 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
         (e = hipMemcpy(c->d_ic, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_qc, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "hipMemcpy defaults");
+    c->h_lo = lo;
+    c->h_bins = bins;
     *out = c;
-    if (mkid_reset_stream(c) != MKID_OK) {
+    if (upload_lo_folded(c) != MKID_OK || mkid_reset_stream(c) != MKID_OK) {
         g_err = c->err;
         free_all(c);
         delete c;
@@ -393,7 +401,10 @@ int mkid_set_bins(mkid_ctx* c, const int32_t* bins, int32_t n) {
     if (n != c->C) FAIL(c, MKID_E_ARG, "need one bin per channel");
     std::vector<int32_t> b(bins, bins + n);
     for (auto& v : b) v = ((v % c->N) + c->N) % c->N;
-    return upload(c, c->d_bins, b.data(), (size_t)n * 4);
+    int r = upload(c, c->d_bins, b.data(), (size_t)n * 4);
+    if (r) return r;
+    c->h_bins = b;
+    return upload_lo_folded(c);
 }
 
 int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
@@ -406,6 +417,20 @@ int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
             const size_t i = (size_t)ch * P + p;
             lo[(size_t)p * c->C + ch] = make_float2(li[i] / 32768.f, -lq[i] / 32768.f);
         }
+    c->h_lo = std::move(lo);
+    return upload_lo_folded(c);
+}
+
+// d_lo[p][c] = h_lo[p][c] * (-1)^(b_c (k+1)) for any frame k = p (mod P): odd bins flip the sign
+// on even rows (P is even). The kernels then multiply by d_lo only.
+static int upload_lo_folded(mkid_ctx* c) {
+    std::vector<float2> lo = c->h_lo;
+    for (int p = 0; p < c->P; p += 2)
+        for (int ch = 0; ch < c->C; ++ch)
+            if (c->h_bins[ch] & 1) {
+                float2& v = lo[(size_t)p * c->C + ch];
+                v = make_float2(-v.x, -v.y);
+            }
     return upload(c, c->d_lo, lo.data(), lo.size() * 8);
 }
 

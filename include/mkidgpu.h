@@ -91,8 +91,12 @@ int mkid_get_cfg(const mkid_ctx* ctx, mkid_cfg* out);
 int mkid_set_stream(mkid_ctx* ctx, void* hip_stream);
 
 /* PFB prototype filter, T*N float coefficients (build decision: the firmware's taps are not in
- * the reference). */
+ * the reference). Applied as 16-bit integers, like an FPGA PFB's fixed-point coefficients:
+ * h_q = rint(h * 2^S) with the largest S such that every point's sum_tau |h_q[tau N + p]| <= 65535
+ * and every |h_q| <= 32767; the effective taps are h_q * 2^-S (mkids_sdr_amd.pfb.effective_taps). */
 int mkid_set_pfb(mkid_ctx* ctx, const float* coeffs, int32_t n);
+/* Host-only (no device needed): the effective taps h_q * 2^-S of mkid_set_pfb and S. */
+int mkid_pfb_effective_taps(const float* coeffs, int32_t T, int32_t N, float* out, int32_t* shift);
 
 /* Coarse FFT bin per channel: replaces write_int('bins'), write_int('load_bins',(i<<1)+1)
  * (ROACH_Setup.py:534-550; ROACH_Pulses.py:958-974). bins[c] in [0,N). */

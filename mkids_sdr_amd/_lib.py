@@ -74,6 +74,7 @@ _SIGS = {
     'mkid_get_cfg': [P, P],
     'mkid_set_stream': [P, P],
     'mkid_set_pfb': [P, P, I32],
+    'mkid_pfb_effective_taps': [P, I32, I32, P, P],
     'mkid_set_bins': [P, P, I32],
     'mkid_set_dds': [P, P, P, I32],
     'mkid_set_lpf': [P, P, I32],
@@ -117,6 +118,8 @@ def load(path=None):
                           '(make -C mkids_sdr_amd/csrc); there is no CPU fallback' % lp)
     L = ctypes.CDLL(lp)
     for name, args in _SIGS.items():
+        if path is not None and not hasattr(L, name):
+            continue  # an older build variant (tools/kbench.py A/B) may predate a symbol
         f = getattr(L, name)
         f.argtypes = args
         f.restype = ctypes.c_int

@@ -7,7 +7,8 @@
 // FPB = 4 frames per iteration (NT = N/8 threads per frame, 8 points per thread):
 //   input  LDS ring of RS = 2T-1+FPB hops of M int16 I/Q samples; each iteration brings 4 new
 //          hops with ONE 16-byte global load per thread, issued one iteration ahead.
-//   PFB    u[p] = sum_tau h[tau N + p] x[(k+1)M - TN + tau N + p]   (h as float4 per p in LDS)
+//   PFB    u[p] = sum_tau h_q[tau N + p] x[(k+1)M - TN + tau N + p]: exact int16 dot products
+//          (taps h_q = rint(h 2^S), mkid_set_pfb; the 2^-S rides in the LO table)
 //   FFT    Stockham radix-8/4 passes through a padded per-frame LDS buffer (fft_common.h); the
 //          last pass is fused into the select: thread c evaluates only the radix-4 butterfly
 //          output X[bin_c] (4 LDS reads, 3 complex MACs with per-channel constant twiddles).
@@ -51,6 +52,9 @@
 
 namespace mkid {
 
+typedef short fshort2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fshort2_t as_s2(uint32_t v) { return __builtin_bit_cast(fshort2_t, v); }
+
 // Radix sequence per FFT length (8 points per thread). The last pass is not run through LDS:
 // its radix-RL butterfly is evaluated only for the selected bin, by the channel's thread.
 template <int N>
@@ -80,7 +84,7 @@ struct FGeo {
     static_assert(NSL % 16 == 0, "pad-linear offsets in the fused last pass");
     using TW2 = TwiddleLds<N, PTS, FPlan<N>::R[1], NS2>;
     using TW3 = TwiddleLds<N, PTS, (FPlan<N>::NP == 4 ? FPlan<N>::R[2] : 2), NS3>;
-    static constexpr size_t tw_offset = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8 + (size_t)N * 16;
+    static constexpr size_t tw_offset = (size_t)RS * M * 4 + (size_t)FPB * LDSF * 8 + (size_t)N * 8;
     static constexpr size_t lds_bytes = tw_offset + (size_t)(TW2::ENTRIES + TW3::ENTRIES) * 8;
     static constexpr int HIST = (2 * T - 1 + kLpfHist) * M;  // ADC history samples
     // register budget sized for 4 waves per SIMD (16 per CU, <= 128 VGPRs): HIP's second
@@ -111,12 +115,12 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     const int slot = tid / NT;  // frame of the iteration this thread transforms
     const int t = tid % NT;
     float2* buf = fbuf + slot * G::LDSF;
-    // PFB taps of point p as one float4 {h[p], h[N+p], h[2N+p], h[3N+p]} in LDS (registers are
-    // the scarce resource at 1024 threads: the low-pass accumulators live there)
-    float4* hl = reinterpret_cast<float4*>(smem + (size_t)RS * M * 4 + (size_t)FPB * G::LDSF * 8);
-    static_assert(T == 4, "one float4 of taps per point");
-    for (int p = tid; p < N; p += G::BT)
-        hl[p] = make_float4(a.pfb[p], a.pfb[N + p], a.pfb[2 * N + p], a.pfb[3 * N + p]);
+    // PFB taps of point p as int16 pairs {h0|h1, h2|h3} in LDS (8 B per point): the PFB is an
+    // exact int16 x int16 dot product per I/Q component (v_dot2_i32_i16), the tap scale 2^-S
+    // rides in the LO table
+    uint2* hl = reinterpret_cast<uint2*>(smem + (size_t)RS * M * 4 + (size_t)FPB * G::LDSF * 8);
+    static_assert(T == 4, "two int16 tap pairs per point");
+    for (int p = tid; p < N; p += G::BT) hl[p] = a.pfbq[p];
 
     // pass-2/3 twiddle tables in LDS (filled once; published by the prologue barrier)
     float2* twt = reinterpret_cast<float2*>(smem + G::tw_offset);
@@ -189,17 +193,24 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         for (int r = 0; r < PTS; ++r) {
             const int p = t + r * NT;
             const int hi = p / M, off = p % M;
-            const float4 h4 = hl[p];
-            const float hh[T] = {h4.x, h4.y, h4.z, h4.w};
-            float ur = 0.f, ui = 0.f;
+            const uint2 hp = hl[p];
+            uint32_t w[T];
 #pragma unroll
             for (int tau = 0; tau < T; ++tau) {
                 int sl = sb + 2 * tau + hi;
                 sl -= sl >= RS ? RS : 0;  // sb + 2 tau + hi < 2 RS
-                const uint32_t w = ring[sl * M + off];
-                ur = fmaf(hh[tau], (float)(int16_t)(w & 0xffffu), ur);
-                ui = fmaf(hh[tau], (float)(int16_t)(w >> 16), ui);
+                w[tau] = ring[sl * M + off];
             }
+            // (I_tau0 | I_tau1 << 16) etc.: low halves are I, high halves Q
+            const uint32_t i01 = __builtin_amdgcn_perm(w[1], w[0], 0x05040100u);
+            const uint32_t q01 = __builtin_amdgcn_perm(w[1], w[0], 0x07060302u);
+            const uint32_t i23 = __builtin_amdgcn_perm(w[3], w[2], 0x05040100u);
+            const uint32_t q23 = __builtin_amdgcn_perm(w[3], w[2], 0x07060302u);
+            int32_t ai = __builtin_amdgcn_sdot2(as_s2(hp.x), as_s2(i01), 0, false);
+            ai = __builtin_amdgcn_sdot2(as_s2(hp.y), as_s2(i23), ai, false);
+            int32_t aq = __builtin_amdgcn_sdot2(as_s2(hp.x), as_s2(q01), 0, false);
+            aq = __builtin_amdgcn_sdot2(as_s2(hp.y), as_s2(q23), aq, false);
+            const float ur = (float)ai, ui = (float)aq;
             v[r] = make_float2(ur, ui);
             // keep the point order: stops the scheduler from hoisting all 32 ring loads at once
             // (register pressure) ...

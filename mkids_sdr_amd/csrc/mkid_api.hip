@@ -52,7 +52,9 @@ struct mkid_ctx {
     int C = 0, N = 0, M = 0, T = 0, P = 0, capc = 0;
     int64_t Kmax = 0, Jmax = 0;
     // configuration
-    float* d_pfb = nullptr;
+    float* d_pfb = nullptr;      // effective taps h_q 2^-S (float, split path)
+    uint2* d_pfbq = nullptr;     // [N] {h_q[0]|h_q[1]<<16, h_q[2]|h_q[3]<<16} (fused path, int16 dot2)
+    int pfb_shift = 0;           // S
     int32_t* d_bins = nullptr;
     float2* d_lo = nullptr;
     int16_t* d_fir = nullptr;
@@ -170,7 +172,7 @@ static int flush_timing(mkid_ctx* c) {
 }
 
 static void free_all(mkid_ctx* c) {
-    void* ptrs[] = {c->d_pfb,   c->d_bins,  c->d_lo,    c->d_fir,    c->d_ic,     c->d_qc,
+    void* ptrs[] = {c->d_pfb,   c->d_pfbq,  c->d_bins,  c->d_lo,    c->d_fir,    c->d_ic,     c->d_qc,
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
@@ -222,7 +224,32 @@ struct DevBufs {
     }
 };
 
+// K1 taps as the device applies them (include/mkidgpu.h, mkid_set_pfb): h_q = rint(h 2^S) int16
+// with the largest S such that every point's four |h_q| sum to <= 65535 and every |h_q| <= 32767
+// (so the fused kernel's int16 dot products never overflow int32 on int16 samples).
+static int quantize_pfb(const float* h, int T, int N, std::vector<int16_t>& hq) {
+    double ms = 0.0, ma = 0.0;
+    for (int p = 0; p < N; ++p) {
+        double sp = 0.0;
+        for (int t = 0; t < T; ++t) {
+            const double a = std::fabs((double)h[t * N + p]);
+            sp += a;
+            ma = std::max(ma, a);
+        }
+        ms = std::max(ms, sp);
+    }
+    int S = 0;
+    if (ms > 0.0) {
+        S = -64;
+        while (S < 64 && std::ldexp(ms, S + 1) <= 65535.0 && std::ldexp(ma, S + 1) <= 32767.0) ++S;
+    }
+    hq.resize((size_t)T * N);
+    for (size_t i = 0; i < hq.size(); ++i) hq[i] = (int16_t)std::rint(std::ldexp((double)h[i], S));
+    return S;
+}
+
 static int upload_lo_folded(mkid_ctx* c);
+static int upload_pfb(mkid_ctx* c, const float* coeffs);
 
 extern "C" {
 
@@ -300,6 +327,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     for (int b = 0; b < 2; ++b)
         if ((e = hipEventRecord(c->ev_zfree[b], c->sB)) != hipSuccess) return fail(e, "hipEventRecord");
     AL(d_pfb, (size_t)c->T * N);
+    AL(d_pfbq, (size_t)N);
     AL(d_bins, C);
     AL(d_lo, (size_t)C * P);
     AL(d_fir, (size_t)C * kFirTaps);
@@ -339,8 +367,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     std::vector<int16_t> fir((size_t)C * kFirTaps, 0);
     std::vector<float> zero(C, 0.f);
     for (int i = 0; i < kFirTaps; ++i) c->lpf.g[i] = kBlackman250k[i] / 2048.0f;
-    if ((e = hipMemcpy(c->d_pfb, h.data(), h.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_bins, bins.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+    if ((e = hipMemcpy(c->d_bins, bins.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_thr, thr.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_lo, lo.data(), lo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_fir, fir.data(), fir.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
@@ -350,7 +377,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->h_lo = lo;
     c->h_bins = bins;
     *out = c;
-    if (upload_lo_folded(c) != MKID_OK || mkid_reset_stream(c) != MKID_OK) {
+    if (upload_pfb(c, h.data()) != MKID_OK || mkid_reset_stream(c) != MKID_OK) {
         g_err = c->err;
         free_all(c);
         delete c;
@@ -390,10 +417,38 @@ static int upload(mkid_ctx* c, void* dst, const void* src, size_t bytes) {
     return MKID_OK;
 }
 
+static int upload_pfb(mkid_ctx* c, const float* coeffs) {
+    const int T = c->T, N = c->N;
+    std::vector<int16_t> hq;
+    const int S = quantize_pfb(coeffs, T, N, hq);
+    std::vector<float> hf(hq.size());
+    for (size_t i = 0; i < hq.size(); ++i) hf[i] = (float)std::ldexp((double)hq[i], -S);
+    std::vector<uint2> hp(N);
+    for (int p = 0; p < N; ++p) {
+        auto u16 = [&](int t) { return (uint32_t)(uint16_t)hq[(size_t)t * N + p]; };
+        hp[p] = make_uint2(u16(0) | (u16(1) << 16), u16(2) | (u16(3) << 16));
+    }
+    int r = upload(c, c->d_pfb, hf.data(), hf.size() * 4);
+    if (r) return r;
+    r = upload(c, c->d_pfbq, hp.data(), hp.size() * 8);
+    if (r) return r;
+    c->pfb_shift = S;
+    return upload_lo_folded(c);  // the fused path folds 2^-S into the LO table
+}
+
+int mkid_pfb_effective_taps(const float* coeffs, int32_t T, int32_t N, float* out, int32_t* shift) {
+    if (!coeffs || !out || T <= 0 || N <= 0) return MKID_E_ARG;
+    std::vector<int16_t> hq;
+    const int S = quantize_pfb(coeffs, T, N, hq);
+    for (size_t i = 0; i < hq.size(); ++i) out[i] = (float)std::ldexp((double)hq[i], -S);
+    if (shift) *shift = S;
+    return MKID_OK;
+}
+
 int mkid_set_pfb(mkid_ctx* c, const float* coeffs, int32_t n) {
     if (!c || !coeffs) return MKID_E_ARG;
     if (n != c->T * c->N) FAIL(c, MKID_E_ARG, "pfb coefficient count must be T*N");
-    return upload(c, c->d_pfb, coeffs, (size_t)n * 4);
+    return upload_pfb(c, coeffs);
 }
 
 int mkid_set_bins(mkid_ctx* c, const int32_t* bins, int32_t n) {
@@ -425,12 +480,14 @@ int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
 // on even rows (P is even). The kernels then multiply by d_lo only.
 static int upload_lo_folded(mkid_ctx* c) {
     std::vector<float2> lo = c->h_lo;
-    for (int p = 0; p < c->P; p += 2)
-        for (int ch = 0; ch < c->C; ++ch)
-            if (c->h_bins[ch] & 1) {
-                float2& v = lo[(size_t)p * c->C + ch];
-                v = make_float2(-v.x, -v.y);
-            }
+    // fused path: the PFB output is the integer h_q . x, so the 2^-S tap scale joins the LO
+    const float sc = c->fused ? (float)std::ldexp(1.0, -c->pfb_shift) : 1.0f;
+    for (int p = 0; p < c->P; ++p)
+        for (int ch = 0; ch < c->C; ++ch) {
+            float2& v = lo[(size_t)p * c->C + ch];
+            const float sg = ((p & 1) == 0 && (c->h_bins[ch] & 1)) ? -sc : sc;
+            v = make_float2(v.x * sg, v.y * sg);
+        }
     return upload(c, c->d_lo, lo.data(), lo.size() * 8);
 }
 
@@ -535,7 +592,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         FrontArgs fa{};
         fa.x = x + off;
         fa.xhist = c->d_xhist;
-        fa.pfb = c->d_pfb;
+        fa.pfbq = c->d_pfbq;
         fa.bins = c->d_bins;
         fa.lo = c->d_lo;
         fa.ic = c->d_ic;

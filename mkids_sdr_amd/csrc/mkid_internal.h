@@ -64,7 +64,7 @@ struct LpfArgs {
 struct FrontArgs {
     const uint32_t* x;      // chunk, int16 I/Q packed per 32-bit word
     const uint32_t* xhist;  // front_hist_samples(N) previous samples
-    const float* pfb;       // T*N prototype
+    const uint2* pfbq;      // [N] int16 taps {h0|h1<<16, h2|h3<<16} of point p (scale 2^S in lo)
     const int32_t* bins;    // C
     const float2* lo;       // [P][C], conj(LUT)/2^15
     const float* ic;        // C

@@ -15,7 +15,7 @@ restatement follows:
   K6  IQ-centre subtract + phase: atan2(Q-Qc, I-Ic) (pulse_triggering_IQ.py:152 host replay),
       quantised to int16 Fix16_13 rad, clamp +-25736 (ROACH_Pulses.py:274-278).
 Build decisions: PFB with T=4 taps per branch, Hamming-windowed sinc prototype
-normalised to unit DC gain; frame k covers samples [(k+1)M - TN, (k+1)M); the 2x-oversampling
+normalised to unit DC gain, applied as 16-bit taps (quantize_pfb, the device's rule); frame k covers samples [(k+1)M - TN, (k+1)M); the 2x-oversampling
 rotation (-1)^(b(k+1)) is removed so a bin-centred tone gives a constant channel output.
 """
 import numpy as np
@@ -33,6 +33,23 @@ def pfb_prototype(N, T=4):
     return h.astype(np.float32)
 
 
+def quantize_pfb(h, T, N):
+    """The taps the device applies (mkid_set_pfb, include/mkidgpu.h): h_q = rint(h 2^S) int16 with
+    the largest S such that every point's sum_tau |h_q| <= 65535 and every |h_q| <= 32767;
+    effective taps h_q 2^-S (exact in float32/float64)."""
+    h = np.asarray(h, np.float32).astype(np.float64).reshape(T, N)
+    ms = float(np.max(np.abs(h[0]) + np.abs(h[1]) + np.abs(h[2]) + np.abs(h[3]))) if T == 4 else \
+        float(np.max(np.abs(h).sum(axis=0)))
+    ma = float(np.max(np.abs(h)))
+    S = 0
+    if ms > 0.0:
+        S = -64
+        while S < 64 and np.ldexp(ms, S + 1) <= 65535.0 and np.ldexp(ma, S + 1) <= 32767.0:
+            S += 1
+    hq = np.rint(np.ldexp(h, S))
+    return np.ldexp(hq, -S).reshape(-1), int(S)
+
+
 def lo_table(lut_i, lut_q):
     """[C][P] int16 LUT -> complex128 conj(LUT)/2^15 (K4 mixer)."""
     return (np.asarray(lut_i, np.float64) - 1j * np.asarray(lut_q, np.float64)) / 32768.0
@@ -47,7 +64,7 @@ class OracleChain:
         self.N = 2 * self.C
         self.M = self.C
         self.T = T
-        self.h = np.asarray(pfb_coeffs, np.float32).astype(np.float64).reshape(T, self.N)
+        self.h = quantize_pfb(pfb_coeffs, T, self.N)[0].reshape(T, self.N)
         self.bins = np.asarray(bins, np.int64) % self.N
         self.lo = lo_table(lut_i, lut_q)
         self.P = self.lo.shape[1]

@@ -195,3 +195,23 @@ def test_lds_layouts_linear():
             assert L.exchange(N, Rw, NS, Rr, p)[0], ('k_channelize', N, name)
     # the conflict-free claim for the headline geometry
     assert L.exchange(2048, 8, 8, 8, L.PADB)[1:] == (32, 16)
+
+
+@pytest.mark.parametrize('N', [128, 512, 2048, 4096])
+def test_pfb_tap_quantisation_matches_oracle(N):
+    """The device's 16-bit PFB tap rule (mkid_pfb_effective_taps, host-only ABI call) equals the
+    oracle's restatement and the product Python mirror, bit for bit."""
+    import ctypes
+    from mkids_sdr_amd import _lib, pfb
+    from oracle.chain import pfb_prototype, quantize_pfb
+    rng = np.random.default_rng(N)
+    for h in (pfb_prototype(N), (rng.normal(size=4 * N) * 1e-3).astype(np.float32)):
+        out = np.empty(4 * N, np.float32)
+        S = ctypes.c_int32()
+        L = _lib.load()
+        assert L.mkid_pfb_effective_taps(h.ctypes.data_as(ctypes.c_void_p), 4, N,
+                                         out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(S)) == 0
+        ref, Sr = quantize_pfb(h, 4, N)
+        mine, Sm = pfb.effective_taps(h)
+        assert S.value == Sr == Sm
+        assert np.array_equal(out.astype(np.float64), ref) and np.array_equal(mine, ref)

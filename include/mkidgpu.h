@@ -123,7 +123,8 @@ int mkid_set_centers(mkid_ctx* ctx, const float* ic, const float* qc, int32_t n)
  * replaces capture_threshold / capture_load_thresh (ROACH_Pulses.py:211-354). */
 int mkid_set_thresholds(mkid_ctx* ctx, const int32_t* thr, int32_t n);
 
-/* Baseline: mode MKID_BASE_*, alpha Fix12_9, kf/kq Fix18_16, base_thr Fix16_13 (0 = no gate). */
+/* Baseline: mode MKID_BASE_*, alpha Fix12_9 in 0..1024 (gain <= 2.0; larger gains diverge),
+ * kf/kq Fix18_16, base_thr Fix16_13 (0 = no gate). */
 int mkid_set_baseline(mkid_ctx* ctx, int32_t mode, int32_t alpha, int32_t kf, int32_t kq,
                       int32_t base_thr);
 

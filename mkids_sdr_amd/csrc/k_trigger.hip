@@ -56,7 +56,8 @@ __device__ __forceinline__ int32_t mf_at(const Win& win, const int32_t (&tap)[kF
 typedef short short2_t __attribute__((ext_vector_type(2)));
 struct QWin {
     uint32_t q[kFirTaps];  // slot (i - base) % 26 holds q_i
-    int32_t last;          // raw_{i-1} for the next pack
+    uint32_t last;         // the dword holding raw_{i-1} (in the lane's half) for the next pack
+    uint32_t sel;          // v_perm selector: (raw_j, raw_{j-1}) from the lane's half of two dwords
 };
 
 __device__ __forceinline__ uint32_t pack2(int32_t lo, int32_t hi) {
@@ -76,11 +77,14 @@ __device__ __forceinline__ void load_qwin(QWin& w, const TrigSpecArgs& a, int c,
         w.q[i] = pack2(r, prev);
         prev = r;
     }
-    w.last = prev;
+    w.last = pack2(prev, prev);   // raw_{j-1} in both halves: valid for either lane parity
+    w.sel = (c & 1) ? 0x07060302u : 0x05040100u;
 }
 
-__device__ __forceinline__ int32_t mf_q(QWin& w, const uint32_t (&tp)[kFirTaps / 2], int u, int32_t r) {
-    w.q[u] = pack2(r, w.last);
+// r: the aligned dword holding raw_j (lanes 2k and 2k+1 load the same dword and keep their own
+// half): the pack is one v_perm, and the loaded values stay 32-bit through the pipelined loop
+__device__ __forceinline__ int32_t mf_q(QWin& w, const uint32_t (&tp)[kFirTaps / 2], int u, uint32_t r) {
+    w.q[u] = __builtin_amdgcn_perm(w.last, r, w.sel);
     w.last = r;
     int32_t acc = 0;
 #pragma unroll
@@ -89,8 +93,59 @@ __device__ __forceinline__ int32_t mf_q(QWin& w, const uint32_t (&tp)[kFirTaps /
     return mf_out(acc);
 }
 
+// Software pipeline over half groups of 13 samples: the loads of the next half are in flight
+// while the current half is processed (26 load registers, as for a whole-group batch, but no
+// wave waits a full memory latency per group). body(group, u, raw) sees u = 0..25 in order;
+// roff advances by ngroups rows of 26. The last prefetch re-reads the current group (in bounds).
+template <class F>
+__device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, uint32_t& roff,
+                                           uint32_t row, F&& body) {
+    constexpr int H = kFirTaps / 2;
+    auto ld = [&](uint32_t off) { return *reinterpret_cast<const uint32_t*>(rbase + off); };
+    uint32_t ra[H], rb[H];
+    if (ngroups <= 0) return;
+#pragma unroll
+    for (int u = 0; u < H; ++u) ra[u] = ld(roff + (uint32_t)u * row);
+    for (int32_t g = 0; g < ngroups; ++g) {
+#pragma unroll
+        for (int u = 0; u < H; ++u) rb[u] = ld(roff + (uint32_t)(H + u) * row);
+#pragma unroll
+        for (int u = 0; u < H; ++u) body(g, u, ra[u]);
+        const uint32_t nxt = roff + (g + 1 < ngroups ? (uint32_t)kFirTaps * row : 0u);
+#pragma unroll
+        for (int u = 0; u < H; ++u) ra[u] = ld(nxt + (uint32_t)u * row);
+#pragma unroll
+        for (int u = 0; u < H; ++u) body(g, H + u, rb[u]);
+        roff += (uint32_t)kFirTaps * row;
+    }
+}
+
+// The per-sample recurrence of k_trig_spec: trig_update itself for SVF (a single exact segment),
+// the code-state form trig_update_fast for EMA / no baseline (the throughput path).
+template <int MODE, bool FAST = (MODE != MKID_BASE_SVF)>
+struct Stepper {
+    TrigState st;
+    TrigCfg k;
+    __device__ Stepper(const TrigState& s, const TrigCfg& kk, int32_t) : st(s), k(kk) {}
+    __device__ __forceinline__ bool step(int32_t f, EvInfo& ev) { return trig_update(st, f, k, ev); }
+    __device__ __forceinline__ TrigState state() const { return st; }
+};
+
 template <int MODE>
-__global__ __launch_bounds__(kSpecThreads) void k_trig_spec(TrigSpecArgs a) {
+struct Stepper<MODE, true> {
+    FastState fs;
+    FastCfg q;
+    // f0: the filtered value of the first sample, which initialises the baseline when the
+    // incoming state has none yet (exactly what trig_update's binit branch does on that sample)
+    __device__ Stepper(const TrigState& s, const TrigCfg& k, int32_t f0) : fs(to_fast(s)), q(fast_cfg(k)) {
+        if (!s.binit) fs.B = MODE == MKID_BASE_NONE ? 0 : f0;
+    }
+    __device__ __forceinline__ bool step(int32_t f, EvInfo& ev) { return trig_update_fast<MODE>(fs, f, q, ev); }
+    __device__ __forceinline__ TrigState state() const { return from_fast(fs); }
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kSpecThreads, 3) void k_trig_spec(TrigSpecArgs a) {
     const int64_t g = (int64_t)blockIdx.x * kSpecThreads + threadIdx.x;
     if (g >= (int64_t)a.C * a.nseg) return;
     const int C = a.C;
@@ -103,7 +158,6 @@ __global__ __launch_bounds__(kSpecThreads) void k_trig_spec(TrigSpecArgs a) {
     const int64_t seg0 = (int64_t)s * a.L;
     const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
     const int64_t jw = s == 0 ? 0 : seg0 - a.W;
-    TrigState st = s == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
     QWin win;
     load_qwin(win, a, c, jw);
     const int64_t sc = (int64_t)c * a.nseg + s;
@@ -112,52 +166,41 @@ __global__ __launch_bounds__(kSpecThreads) void k_trig_spec(TrigSpecArgs a) {
     // all lanes of a wave share the segment (64 | C): a scalar row base and a 32-bit per-lane
     // offset give SGPR-base loads (no 64-bit address arithmetic per sample)
     const char* rbase = reinterpret_cast<const char*>(a.raw + (int64_t)__builtin_amdgcn_readfirstlane((int32_t)jw) * C);
-    uint32_t roff = (uint32_t)c * 2u;  // byte offset (a 32-bit VGPR next to an SGPR base)
-    auto rload = [&](uint32_t off) { return (int32_t)*reinterpret_cast<const int16_t*>(rbase + off); };
+    uint32_t roff = (uint32_t)(c >> 1) * 4u;  // byte offset of the lane's dword (C even)
+    auto rload = [&](uint32_t off) { return *reinterpret_cast<const uint32_t*>(rbase + off); };
+    QWin w0 = win;
+    Stepper<MODE> sp(s == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0}, k,
+                     mf_q(w0, tp, 0, rload(roff)));
     // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0
-    for (int32_t gi = 0; gi < (int32_t)(seg0 - jw); gi += kFirTaps) {
-        int32_t r[kFirTaps];
-#pragma unroll
-        for (int u = 0; u < kFirTaps; ++u) r[u] = rload(roff + (uint32_t)(2 * u * C));  // all loads in flight
-        roff += (uint32_t)(2 * kFirTaps * C);
-#pragma unroll
-        for (int u = 0; u < kFirTaps; ++u) {
-            EvInfo ev;
-            (void)trig_update(st, mf_q(win, tp, u, r[u]), k, ev);
-        }
-    }
-    if (s > 0) a.s_spec[(int64_t)s * C + c] = st;
+    run_groups(__builtin_amdgcn_readfirstlane((int32_t)(seg0 - jw) / kFirTaps), rbase, roff, (uint32_t)(2 * C), [&](int32_t, int u, uint32_t r) {
+        EvInfo ev;
+        (void)sp.step(mf_q(win, tp, u, r), ev);
+    });
+    if (s > 0) a.s_spec[(int64_t)s * C + c] = sp.state();
     const int32_t len = (int32_t)(seg1 - seg0);
     const int32_t full = len - len % kFirTaps;
-    int32_t gi = 0;
-    for (; gi < full; gi += kFirTaps) {
-        int32_t r[kFirTaps];
-#pragma unroll
-        for (int u = 0; u < kFirTaps; ++u) r[u] = rload(roff + (uint32_t)(2 * u * C));
-        roff += (uint32_t)(2 * kFirTaps * C);
-#pragma unroll
-        for (int u = 0; u < kFirTaps; ++u) {
-            const int32_t f = mf_q(win, tp, u, r[u]);
-            EvInfo ev;
-            if (trig_update(st, f, k, ev)) {
-                if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);
-                ++n;
-            }
+    run_groups(__builtin_amdgcn_readfirstlane(full / kFirTaps), rbase, roff, (uint32_t)(2 * C), [&](int32_t gr, int u, uint32_t r) {
+        const int32_t f = mf_q(win, tp, u, r);
+        EvInfo ev;
+        if (sp.step(f, ev)) {
+            if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gr * kFirTaps + u);
+            ++n;
         }
-    }
+    });
+    const int32_t gi = full;
     const int32_t left = len - gi;  // tail < 26 samples, predicated
 #pragma unroll
     for (int u = 0; u < kFirTaps; ++u) {
         if (u < left) {
             const int32_t f = mf_q(win, tp, u, rload(roff + (uint32_t)(2 * u * C)));
             EvInfo ev;
-            if (trig_update(st, f, k, ev)) {
+            if (sp.step(f, ev)) {
                 if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);
                 ++n;
             }
         }
     }
-    a.s_end[(int64_t)s * C + c] = st;
+    a.s_end[(int64_t)s * C + c] = sp.state();
     a.counts[sc] = n;
 }
 
@@ -176,12 +219,17 @@ __device__ bool rerun_segment(const TrigSpecArgs& a, int c, int s, const int32_t
     const int16_t* rp = a.raw + seg0 * a.C + c;
     for (int64_t g = seg0; g < seg1 && !merged; g += kFirTaps) {
         const int64_t left = seg1 - g;
+        // one latency per 26 samples: the group's loads are issued before the merge test can
+        // stop the walk (a serial walk otherwise waits on every load)
+        int32_t r[kFirTaps];
+#pragma unroll
+        for (int u = 0; u < kFirTaps; ++u) r[u] = u < left ? rp[(int64_t)u * a.C] : 0;
+        rp += (int64_t)kFirTaps * a.C;
 #pragma unroll
         for (int u = 0; u < kFirTaps; ++u) {
             if (u >= left || merged) continue;
             const int64_t j = g + u;
-            win.w[u] = *rp;
-            rp += a.C;
+            win.w[u] = r[u];
             const int32_t f = mf_at(win, tap, u);
             uint64_t pkt;
             if (trig_step(tru, f, k, c, a.j0 + j, &pkt)) {
@@ -259,6 +307,16 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
     }
     a.st_out[c] = override_ ? T : a.s_end[(int64_t)(a.nseg - 1) * C + c];
     if (a.reruns) a.reruns[c] = reruns;
+}
+
+int64_t trigger_wave_slots(int device) {
+    int ncu = 0, nb = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trig_spec<MKID_BASE_EMA>, kSpecThreads, 0) != hipSuccess ||
+        nb <= 0)
+        nb = 1;
+    return (int64_t)ncu * nb * (kSpecThreads / 64);
 }
 
 hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s) {

@@ -5,6 +5,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -28,9 +29,11 @@ struct KTime {
     hipEvent_t a, b;
 };
 
-// Speculative trigger segmentation (k_trigger.hip): segments of kSegL phase samples, each
-// speculating from kSegW samples of warm-up. The EMA baseline (alpha 41/512) forgets its start
-// in ~10^2 samples on noisy phase; SVF runs as a single exact segment.
+// Speculative trigger segmentation (k_trigger.hip): segments of at least kSegL phase samples,
+// each speculating from kSegW samples of warm-up. The EMA baseline (alpha 41/512) forgets its
+// start in ~10^2 samples on noisy phase; SVF runs as a single exact segment. A long call uses
+// longer segments so that the (channel, segment) waves fit the GPU's resident wave slots in one
+// round (less warm-up per sample, no tail round).
 #ifndef MKID_SEG_L
 #define MKID_SEG_L 2048
 #endif
@@ -40,7 +43,13 @@ struct KTime {
 constexpr int64_t kSegL = MKID_SEG_L;
 constexpr int64_t kSegW = MKID_SEG_W;  // multiple of the 26-sample matched-filter ring
 static_assert(kSegW % kFirTaps == 0 && kSegL >= kSegW + kRawHist, "segment geometry");
-int64_t seg_capacity(int dead) { return kSegL / (dead + 3) + 2; }
+int64_t seg_capacity(int64_t L, int dead) { return L / (dead + 3) + 2; }
+
+// segment length for J rows: >= kSegL, and (C/64) * ceil(J/L) waves <= the resident slots
+int64_t seg_length(int64_t J, int C, int64_t wave_slots) {
+    const int64_t nt = std::max<int64_t>(1, wave_slots * 64 / C);
+    return std::max<int64_t>(kSegL, (J + nt - 1) / nt);
+}
 
 }  // namespace
 
@@ -87,7 +96,7 @@ struct mkid_ctx {
     TrigState *d_sspec = nullptr, *d_send = nullptr;  // [nseg][C]
     uint64_t* d_scratch = nullptr;   // [C][capseg]
     int32_t* d_reruns = nullptr;     // [C]
-    int64_t nseg_max = 0, slot_cap = 0, scratch_cap = 0;
+    int64_t nseg_max = 0, slot_cap = 0, scratch_cap = 0, trig_slots = 0;
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
     int64_t last_J = 0;     // phase rows of the last call
     int64_t last_subJ = 0;  // rows of its last sub-chunk (held in d_raw)
@@ -304,8 +313,13 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     // peak, dead time, re-arm), so no per-channel/segment overflow can occur.
     const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // whole call, one segment
     c->capc = (int)std::min<int64_t>(cfg->max_events_per_ch > 0 ? cfg->max_events_per_ch : cap_bound, INT_MAX / 2);
-    c->nseg_max = (c->Jmax + kSegL - 1) / kSegL;
-    const int64_t capseg = seg_capacity(cfg->dead_time);
+    c->trig_slots = trigger_wave_slots(device);
+    // tuning/test knob: pretend the GPU holds this many trigger waves (forces longer segments)
+    if (const char* ev = getenv("MKID_TRIG_WAVE_SLOTS")) c->trig_slots = std::max<int64_t>(1, atoll(ev));
+    const int64_t Lmax = seg_length(c->Jmax, C, c->trig_slots);
+    // for J <= Jmax: L(J) <= Lmax and ceil(J / L(J)) <= max(slots * 64 / C, ceil(Jmax / kSegL))
+    c->nseg_max = std::max<int64_t>(std::max<int64_t>(1, c->trig_slots * 64 / C), (c->Jmax + kSegL - 1) / kSegL);
+    const int64_t capseg = seg_capacity(Lmax, cfg->dead_time);
     c->slot_cap = std::max<int64_t>((int64_t)C * c->nseg_max * capseg, (int64_t)C * c->capc);
     c->scratch_cap = std::max<int64_t>(capseg, c->capc);
     c->H = c->fused ? front_hist_samples(N) : (int64_t)c->T * N - c->M;
@@ -522,7 +536,8 @@ int mkid_set_thresholds(mkid_ctx* c, const int32_t* thr, int32_t n) {
 int mkid_set_baseline(mkid_ctx* c, int32_t mode, int32_t alpha, int32_t kf, int32_t kq, int32_t base_thr) {
     if (!c) return MKID_E_ARG;
     if (mode < MKID_BASE_NONE || mode > MKID_BASE_SVF) FAIL(c, MKID_E_ARG, "bad baseline mode");
-    if (alpha < 0 || alpha > 4095) FAIL(c, MKID_E_ARG, "alpha must be Fix12_9 (0..4095)");
+    // Fix12_9; above 2.0 (1024) the EMA diverges and its int32 arithmetic overflows
+    if (alpha < 0 || alpha > 1024) FAIL(c, MKID_E_ARG, "alpha must be Fix12_9 in 0..1024 (gain <= 2.0)");
     if (kf < 0 || kf >= (1 << 18) || kq < 0 || kq >= (1 << 18)) FAIL(c, MKID_E_ARG, "kf/kq must be Fix18_16");
     if (base_thr < 0 || base_thr > 65535) FAIL(c, MKID_E_ARG, "base_thr must be Fix16_13 (0..65535)");
     c->mode = mode; c->alpha = alpha; c->kf = kf; c->kq = kq; c->base_thr = base_thr;
@@ -553,10 +568,11 @@ static int run_trigger(mkid_ctx* c, int64_t J, uint64_t* d_events, int64_t cap, 
     const int C = c->C;
     KTime kt;
     const bool serial = c->mode == MKID_BASE_SVF || J <= kSegL;
-    const int32_t L = serial ? (int32_t)J : (int32_t)kSegL;
+    const int64_t Ls = serial ? J : seg_length(J, C, c->trig_slots);
+    const int32_t L = (int32_t)Ls;
     const int32_t W = serial ? 0 : (int32_t)kSegW;
-    const int32_t nseg = serial ? 1 : (int32_t)((J + kSegL - 1) / kSegL);
-    const int32_t capseg = serial ? (int32_t)(J / (c->cfg.dead_time + 3) + 2) : (int32_t)seg_capacity(c->cfg.dead_time);
+    const int32_t nseg = (int32_t)((J + Ls - 1) / Ls);
+    const int32_t capseg = (int32_t)seg_capacity(Ls, c->cfg.dead_time);
     TrigSpecArgs ta{c->d_raw,   c->d_rhist, c->d_fir,  c->d_thr,     c->d_tstate,  c->d_tstate,
                     c->d_sspec, c->d_send,  c->d_slots, c->d_chcounts, c->d_scratch, c->d_reruns,
                     J,          c->j0,      C,          nseg,          L,            W,

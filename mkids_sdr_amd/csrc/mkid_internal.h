@@ -107,6 +107,8 @@ hipError_t launch_channelize(int N, const ChanArgs& a, hipStream_t s);
 hipError_t launch_lpf_phase(const LpfArgs& a, hipStream_t s);
 hipError_t launch_front(int N, const FrontArgs& a, hipStream_t s);
 hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s);
+// resident wave slots of the speculative trigger kernel on a device (occupancy x CUs)
+int64_t trigger_wave_slots(int device);
 hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
                           int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
                           int64_t* scan_ws, hipStream_t s);

@@ -76,6 +76,59 @@ __device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigC
     return emit;
 }
 
+// Hot-loop form of trig_update for the EMA and no-baseline modes (k_trig_spec), same outputs:
+//  * the state machine is one code x: ARMED -1, PULSE -2, REARM 0, DEAD = dead-time samples
+//    left (>= 1). ARMED/REARM share one rule (x' = e < thr ? 2x : -1), DEAD counts down into
+//    REARM, PULSE emits into DEAD max(dead, 1) (a DEAD count <= 0 behaves exactly like 1);
+//  * the baseline is already initialised (binit is settled once before the loop);
+//  * the dead-band gate |e| < base_thr is one unsigned compare (goff/glim), and alpha * e a
+//    24-bit multiply (alpha <= 1024 keeps |e| < 2^18: exact).
+struct FastState {
+    int32_t B, x, f1, f2;
+};
+struct FastCfg {
+    int32_t thr, alpha, dx;
+    uint32_t goff, glim;
+};
+
+__device__ __forceinline__ FastCfg fast_cfg(const TrigCfg& k) {
+    FastCfg q{k.thr, k.alpha, k.dead > 1 ? k.dead : 1, 0x80000000u, 0xffffffffu};
+    if (k.base_thr > 0) {
+        q.goff = (uint32_t)k.base_thr - 1u;
+        q.glim = 2u * (uint32_t)k.base_thr - 1u;
+    }
+    return q;
+}
+
+__device__ __forceinline__ FastState to_fast(const TrigState& s) {
+    const int32_t x = s.st == ST_ARMED ? -1 : (s.st == ST_PULSE ? -2 : (s.st == ST_REARM ? 0 : (s.cnt > 1 ? s.cnt : 1)));
+    return FastState{s.B, x, s.f1, s.f2};
+}
+
+__device__ __forceinline__ TrigState from_fast(const FastState& f) {
+    const int32_t st = f.x == -1 ? ST_ARMED : (f.x == -2 ? ST_PULSE : (f.x == 0 ? ST_REARM : ST_DEAD));
+    return TrigState{f.B, 1, st, f.x > 0 ? f.x : 0, f.f1, f.f2, 0, 0, 0, 0};
+}
+
+template <int MODE>
+__device__ __forceinline__ bool trig_update_fast(FastState& s, int32_t f, const FastCfg& k, EvInfo& ev) {
+    const int32_t e = f - s.B;
+    ev = EvInfo{s.f2, s.f1, s.B};
+    if (MODE == MKID_BASE_EMA) {
+        const bool gate = (uint32_t)e + k.goff < k.glim;
+        s.B += gate ? (__mul24(k.alpha, e) >> 9) : 0;
+    }
+    const int32_t x = s.x;
+    const bool emit = (x == -2) & (f > s.f1);
+    int32_t xn = e < k.thr ? 2 * x : -1;
+    xn = x == -2 ? (f > s.f1 ? k.dx : -2) : xn;
+    xn = x > 0 ? x - 1 : xn;
+    s.x = xn;
+    s.f2 = s.f1;
+    s.f1 = f;
+    return emit;
+}
+
 // Advance state s by one filtered sample f taken at global phase index jg. Returns true and fills
 // *pkt when a packet is emitted (its timestamp is jg - 1: the peak is the previous sample).
 __device__ __forceinline__ bool trig_step(TrigState& s, int32_t f, const TrigCfg& k, int32_t c,

@@ -176,19 +176,25 @@ def test_deleted_channels_and_dead_time(gpu):
     compare(case, thr, [0, S], dead=200)
 
 
-@pytest.mark.parametrize('noise,rate,seed', [
-    (30.0, 1 / 300.0, 51),   # noisy phase: speculation mostly right, pulses straddle segments
-    (0.0, 1 / 200.0, 52),    # noiseless: EMA dead band -> speculation fails -> exact fix-up runs
-    (30.0, 1 / 60.0, 53),    # pile-up: pulses every ~60 samples
+@pytest.mark.parametrize('noise,rate,seed,slots', [
+    (30.0, 1 / 300.0, 51, None),   # noisy phase: speculation mostly right, pulses straddle segments
+    (0.0, 1 / 200.0, 52, None),    # noiseless: EMA dead band -> speculation fails -> exact fix-up
+    (30.0, 1 / 60.0, 53, None),    # pile-up: pulses every ~60 samples
+    (30.0, 1 / 300.0, 54, 3),      # occupancy-sized segments: 3 of 5462 samples (ragged tails)
+    (0.0, 1 / 200.0, 55, 3),
 ])
-def test_speculative_trigger_exact(gpu, noise, rate, seed):
+def test_speculative_trigger_exact(gpu, monkeypatch, noise, rate, seed, slots):
     """Calls long enough (J > 2048 phase samples) to take the parallel speculative-segment
-    trigger; packets must equal the sequential oracle's bit for bit."""
+    trigger; packets must equal the sequential oracle's bit for bit. `slots` pretends the GPU
+    holds that many trigger waves, which stretches the segments beyond the 2048-sample minimum
+    (the path a 2^30-sample call takes on the real chip)."""
     from mkids_sdr_amd.channelizer import Channelizer
     C, S = 64, 2 ** 21
     J = S // (2 * C)
     case = signals.make_case(C, S, seed=seed, noise=noise, pulses_per_ch=J * rate)
     thr = quiet_thresholds(C, 2 ** 18, seed) if noise > 0 else np.full(C, -1200)
+    if slots is not None:
+        monkeypatch.setenv('MKID_TRIG_WAVE_SLOTS', str(slots))
     ch = Channelizer(C, max_chunk=S)
     try:
         configure(ch, case, thr)

@@ -54,6 +54,13 @@ namespace mkid {
 
 typedef short fshort2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ fshort2_t as_s2(uint32_t v) { return __builtin_bit_cast(fshort2_t, v); }
+// First dot product of a chain: the VOP3P form with an inline-constant zero accumulator (the
+// compiler otherwise picks v_dot2c_i32_i16 behind a v_mov of 0)
+__device__ __forceinline__ int32_t dot2_i16_first(uint32_t h, uint32_t x) {
+    int32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(h), "v"(x));
+    return d;
+}
 
 // Radix sequence per FFT length (8 points per thread). The last pass is not run through LDS:
 // its radix-RL butterfly is evaluated only for the selected bin, by the channel's thread.
@@ -112,7 +119,9 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     float2* fbuf = reinterpret_cast<float2*>(smem + (size_t)RS * M * 4);
 
     const int tid = threadIdx.x;
-    const int slot = tid / NT;  // frame of the iteration this thread transforms
+    // frame of the iteration this thread transforms: wave-uniform when a wave lies within one
+    // frame (NT >= 64), so the ring-slot arithmetic below runs on the scalar unit
+    const int slot = NT % 64 == 0 ? __builtin_amdgcn_readfirstlane(tid / NT) : tid / NT;
     const int t = tid % NT;
     float2* buf = fbuf + slot * G::LDSF;
     // PFB taps of point p as int16 pairs {h0|h1, h2|h3} in LDS (8 B per point): the PFB is an
@@ -172,10 +181,20 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     for (int m = 0; m < 13; ++m) acc[m] = make_float2(0.f, 0.f);
     float2 ys = make_float2(0.f, 0.f);
 
+    // 32-bit stream counters, advanced by FPB per iteration (no 64-bit modulo in the loop):
+    //   rb  = ring slot of hop kb + 1 - 2T (the oldest hop frame kb reads); the FPB hops loaded
+    //         for the next iteration, kb + FPB + q = (kb + 1 - 2T) + RS + q, go to slot rb + q
+    //   lrow = LO-table row of frame kb;  kr = kb - k_b (frame index relative to the run)
+    int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);
+    int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
+    const int nrun = (int)(k_e - k_b);
+    const int qh = (tid * G::SPT) / M, qoff = (tid * G::SPT) % M;  // this thread's ring write
+
 #ifdef MKID_XP_STAMPS
     int it_ = 0;
 #endif
-    for (int64_t kb = k_start; kb < k_e; kb += FPB) {
+    for (int kr = -kLpfHist; kr < nrun; kr += FPB) {
+        const int64_t kb = k_b + kr;
 #ifdef MKID_XP_STAMPS
         ++it_;
         STAMP(14);
@@ -183,11 +202,11 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         // LO rows of this iteration's frames (latency hidden behind the FFT)
         float2 lov[FPB];
 #pragma unroll
-        for (int f = 0; f < FPB; ++f) lov[f] = a.lo[((int)(a.k0 + kb + f) & (a.P - 1)) * C + c];
+        for (int f = 0; f < FPB; ++f) lov[f] = (a.lo + ((lrow + f) & (a.P - 1)) * C)[c];
 
         // ---- PFB of frame kb + slot from the LDS ring ----
-        const int64_t h_first = kb + slot + 1 - 2 * T;
-        const int sb = (int)(((h_first % RS) + RS) % RS);
+        int sb = rb + slot;
+        sb -= sb >= RS ? RS : 0;
         float2 v[PTS];
 #pragma unroll
         for (int r = 0; r < PTS; ++r) {
@@ -206,9 +225,9 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
             const uint32_t q01 = __builtin_amdgcn_perm(w[1], w[0], 0x07060302u);
             const uint32_t i23 = __builtin_amdgcn_perm(w[3], w[2], 0x05040100u);
             const uint32_t q23 = __builtin_amdgcn_perm(w[3], w[2], 0x07060302u);
-            int32_t ai = __builtin_amdgcn_sdot2(as_s2(hp.x), as_s2(i01), 0, false);
+            int32_t ai = dot2_i16_first(hp.x, i01);
             ai = __builtin_amdgcn_sdot2(as_s2(hp.y), as_s2(i23), ai, false);
-            int32_t aq = __builtin_amdgcn_sdot2(as_s2(hp.x), as_s2(q01), 0, false);
+            int32_t aq = dot2_i16_first(hp.x, q01);
             aq = __builtin_amdgcn_sdot2(as_s2(hp.y), as_s2(q23), aq, false);
             const float ur = (float)ai, ui = (float)aq;
             v[r] = make_float2(ur, ui);
@@ -221,9 +240,13 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         st_dft<PTS, PL::R[0]>(v);
         FSYNC(0);  // ring reads of this iteration and last iteration's select are done
         {
-            const int64_t hop = kb + FPB + (tid * G::SPT) / M;
-            *reinterpret_cast<uint4*>(ring + (int)(((hop % RS) + RS) % RS) * M + (tid * G::SPT) % M) = pre;
+            int ws = rb + qh;
+            ws -= ws >= RS ? RS : 0;
+            *reinterpret_cast<uint4*>(ring + ws * M + qoff) = pre;
             pre = front_load<N>(a, kb + 2 * FPB, tid);
+            rb += FPB;
+            rb -= rb >= RS ? RS : 0;
+            lrow += FPB;
         }
         st_write<N, PTS, PL::R[0], 1>(buf, v, t);
         FSYNC(1);
@@ -248,7 +271,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         // ---- select + DDC + low-pass + phase for channel c over the FPB frames ----
 #pragma unroll
         for (int f = 0; f < FPB; ++f) {
-            const int64_t k = kb + f;
+            const int kf = kr + f;  // frame kb + f relative to k_b
             const float2* yf = fbuf + f * G::LDSF + yoff;
             float2 X = yf[0];
 #pragma unroll
@@ -281,17 +304,17 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
 #pragma unroll
                 for (int m = 0; m < 12; ++m) acc[m] = acc[m + 1];
                 acc[12] = make_float2(0.f, 0.f);
-                if (k > k_b && k < k_e) {
-                    const int jr = (int)((k - 1 - k_b) >> 1);  // row within the run
+                if (kf > 0 && kf < nrun) {
+                    const int jr = (kf - 1) >> 1;  // row within the run
                     ys.x += y.x;
                     ys.y += y.y;
                     const float ph = phase_atan2(y.y - qc, y.x - ic);
                     int q = __float2int_rn(ph * 8192.0f);
                     q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
 #ifndef MKID_XP_STAMPS
-                    if (phase_run) phase_run[jr * C + c] = ph;
+                    if (phase_run) (phase_run + jr * C)[c] = ph;
 #endif
-                    raw_run[jr * C + c] = (int16_t)q;
+                    (raw_run + jr * C)[c] = (int16_t)q;
                     if (c == a.iq_ch && a.iqtap) {  // IQ snapshot tap (conv_phase_snapIQ_bram)
                         a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y.x);
                         a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y.y);
@@ -301,8 +324,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         }
     }
     if (a.ysum) {
-        atomicAdd(&a.ysum[c].x, ys.x);
-        atomicAdd(&a.ysum[c].y, ys.y);
+        ysum_add(a.ysum, c, ys.x, ys.y);
     }
 }
 

@@ -66,8 +66,7 @@ __global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
         }
     }
     if (a.ysum) {
-        atomicAdd(&a.ysum[c].x, ys.x);
-        atomicAdd(&a.ysum[c].y, ys.y);
+        ysum_add(a.ysum, c, ys.x, ys.y);
     }
 }
 

@@ -89,7 +89,7 @@ struct mkid_ctx {
     // workspace
     float2* d_zb[2] = {nullptr, nullptr};
     int16_t* d_raw = nullptr;
-    float2* d_ysum = nullptr;
+    long long* d_ysum = nullptr;   // [C][2] fixed point 2^-kYsumFrac
     uint64_t* d_slots = nullptr;     // [C][nseg][capseg]
     int32_t* d_chcounts = nullptr;   // [C][nseg]
     int64_t* d_scan = nullptr;       // [C][nseg]
@@ -361,7 +361,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     }
     AL(d_raw, (size_t)c->Jmax * C);
     AL(d_iqtap, (size_t)(cfg->max_chunk / N) * 2);
-    AL(d_ysum, C);
+    AL(d_ysum, (size_t)2 * C);
     AL(d_slots, (size_t)c->slot_cap);
     AL(d_chcounts, (size_t)C * c->nseg_max);
     AL(d_scan, (size_t)C * c->nseg_max + 64);  // >= 3 int64 per compaction tile
@@ -552,7 +552,7 @@ int mkid_reset_stream(mkid_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->d_zhist, 0, (size_t)kLpfHist * c->C * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_rhist, 0, (size_t)kRawHist * c->C * 2, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_tstate, 0, (size_t)c->C * sizeof(TrigState), c->stream));
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 16, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->k0 = 0;
     c->j0 = 0;
@@ -598,7 +598,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     const int C = c->C, N = c->N, M = c->M;
     hipStream_t s = c->stream;
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 8, s));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, s));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
     for (int64_t off = 0; off < n; off += c->G) {
@@ -653,7 +653,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     HIPCHK(c, hipEventRecord(c->ev_start, A));
     HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, B));
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 8, B));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, B));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
     const float2* zprev = c->d_zhist;  // the 24 frames before the current sub-chunk
@@ -806,13 +806,14 @@ int mkid_trigger_reruns(mkid_ctx* c, int64_t* total) {
 int mkid_avg_iq(mkid_ctx* c, float* mi, float* mq) {
     if (!c || !mi || !mq) return MKID_E_ARG;
     if (c->last_J <= 0) FAIL(c, MKID_E_STATE, "no data processed yet");
-    std::vector<float2> s(c->C);
+    std::vector<long long> s(2 * (size_t)c->C);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpyAsync(s.data(), c->d_ysum, (size_t)c->C * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(s.data(), c->d_ysum, (size_t)c->C * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    const double scale = 1.0 / ((double)(1 << kYsumFrac) * (double)c->last_J);
     for (int i = 0; i < c->C; ++i) {
-        mi[i] = (float)(s[i].x / (double)c->last_J);
-        mq[i] = (float)(s[i].y / (double)c->last_J);
+        mi[i] = (float)((double)s[2 * i] * scale);
+        mq[i] = (float)((double)s[2 * i + 1] * scale);
     }
     return MKID_OK;
 }

@@ -53,13 +53,24 @@ struct LpfArgs {
     const float* qc;        // C
     float* phase;           // [J][C] or nullptr
     int16_t* raw;           // [J][C]
-    float2* ysum;           // [C] per-channel sum of y (avgIQ) or nullptr
+    long long* ysum;        // [C][2] per-channel sum of y (avgIQ), fixed point 2^-kYsumFrac, or nullptr
     int64_t J;
     int32_t C;
     LpfTaps taps;
     int16_t* iqtap;         // [J][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
     int32_t iq_ch;
 };
+
+// avgIQ accumulator (firmware K9, avgIQ_bram): per-thread float partial sums are rounded to
+// fixed point (2^-8) and added with integer atomics, so the sums do not depend on the order in
+// which workgroups finish (float atomics would make the loop calibration run-to-run different)
+constexpr int kYsumFrac = 8;
+__device__ __forceinline__ void ysum_add(long long* ysum, int c, float sx, float sy) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(ysum) + 2 * c,
+              (unsigned long long)llrintf(sx * (float)(1 << kYsumFrac)));
+    atomicAdd(reinterpret_cast<unsigned long long*>(ysum) + 2 * c + 1,
+              (unsigned long long)llrintf(sy * (float)(1 << kYsumFrac)));
+}
 
 struct FrontArgs {
     const uint32_t* x;      // chunk, int16 I/Q packed per 32-bit word
@@ -71,7 +82,7 @@ struct FrontArgs {
     const float* qc;        // C
     float* phase;           // [K/2][C] or nullptr
     int16_t* raw;           // [K/2][C]
-    float2* ysum;           // [C] or nullptr
+    long long* ysum;        // [C][2] fixed point 2^-kYsumFrac, or nullptr
     int64_t K;              // frames in this chunk (even)
     int64_t k0;             // global index of the chunk's first frame
     int64_t frames_per_block;  // set by the launcher

@@ -12,6 +12,44 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 }
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // -i * a
 
+// Packed-FP32 forms of the rotations by -+i: one v_pk_add_f32 whose op_sel swaps the halves of
+// the second operand (the compiler otherwise materialises the swap with v_mov pairs).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v f2v_of(float2 a) { return f2v{a.x, a.y}; }
+__device__ __forceinline__ float2 float2_of(f2v a) { return make_float2(a.x, a.y); }
+// a + (-i) b = (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ float2 add_mi(float2 a, float2 b) {
+    f2v d;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(d) : "v"(f2v_of(a)), "v"(f2v_of(b)));
+    return float2_of(d);
+}
+// a - (-i) b = a + i b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ float2 sub_mi(float2 a, float2 b) {
+    f2v d;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(d) : "v"(f2v_of(a)), "v"(f2v_of(b)));
+    return float2_of(d);
+}
+// (a.x + a.y, a.y - a.x) = (1 - i) a   (the W8 rotations up to a real scale)
+__device__ __forceinline__ float2 rot_1mi(float2 a) {
+    f2v d;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(d) : "v"(f2v_of(a)));
+    return float2_of(d);
+}
+// x + s * a for a real scalar s (one v_pk_fma_f32, s broadcast to both halves)
+__device__ __forceinline__ float2 fma_s(float2 a, float s, float2 x) {
+    f2v d;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(f2v_of(a)), "v"(f2v{s, s}), "v"(f2v_of(x)));
+    return float2_of(d);
+}
+// x + t * y (complex multiply-accumulate as two v_pk_fma_f32)
+__device__ __forceinline__ float2 cmac(float2 x, float2 t, float2 y) {
+    f2v d;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+        : "=&v"(d) : "v"(f2v_of(y)), "v"(f2v_of(t)), "v"(f2v_of(x)));
+    return float2_of(d);
+}
+
 __device__ __forceinline__ void dft2(float2& a, float2& b) {
     float2 t = a;
     a = cadd(t, b);
@@ -19,12 +57,12 @@ __device__ __forceinline__ void dft2(float2& a, float2& b) {
 }
 
 __device__ __forceinline__ void dft4(float2& v0, float2& v1, float2& v2, float2& v3) {
-    float2 s02 = cadd(v0, v2), d02 = csub(v0, v2);
-    float2 s13 = cadd(v1, v3), d13 = mul_mi(csub(v1, v3));
+    const float2 s02 = cadd(v0, v2), d02 = csub(v0, v2);
+    const float2 s13 = cadd(v1, v3), t13 = csub(v1, v3);
     v0 = cadd(s02, s13);
     v2 = csub(s02, s13);
-    v1 = cadd(d02, d13);
-    v3 = csub(d02, d13);
+    v1 = add_mi(d02, t13);  // d02 + (-i) t13
+    v3 = sub_mi(d02, t13);
 }
 
 template <int R>
@@ -43,13 +81,13 @@ __device__ __forceinline__ void dft<8>(float2* v) {
     float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
     dft4(e0, e1, e2, e3);
     dft4(o0, o1, o2, o3);
-    o1 = make_float2((o1.x + o1.y) * r2, (o1.y - o1.x) * r2);   // * W8^1
-    o2 = mul_mi(o2);                                           // * W8^2
-    o3 = make_float2((o3.y - o3.x) * r2, -(o3.x + o3.y) * r2);  // * W8^3
+    // W8^1 o1 = r2 (1 - i) o1;  W8^2 o2 = -i o2;  W8^3 o3 = -i r2 (1 - i) o3
+    const float2 p1 = rot_1mi(o1);
+    const float2 p3 = make_float2(rot_1mi(o3).x * r2, rot_1mi(o3).y * r2);
     v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
-    v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
-    v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
-    v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
+    v[1] = fma_s(p1, r2, e1); v[5] = fma_s(p1, -r2, e1);
+    v[2] = add_mi(e2, o2); v[6] = sub_mi(e2, o2);
+    v[3] = add_mi(e3, p3); v[7] = sub_mi(e3, p3);
 }
 
 // LDS index padding: one float2 of pad every 16 entries (breaks power-of-two lane strides).
@@ -170,9 +208,10 @@ struct TwiddleRec {
     }
 };
 
-// Twiddles of one pass read from an LDS table (entry m = j mod NS holds w^1..w^(R-1),
-// w = exp(-2 pi i m / (NS R)), 8 B each, stride (R-1) float2: conflict-free ds_read_b64 for
-// consecutive m, broadcast for NS < 64) instead of being rebuilt by complex multiplies.
+// Twiddles of one pass read from an LDS table: w^r, w = exp(-2 pi i m / (NS R)), m = j mod NS,
+// stored plane by plane (entry (r, m) at (r - 1) NS + m, 8 B each), so consecutive m are
+// consecutive float2: conflict-free ds_read_b64 (2 LDS cycles each; broadcast for NS < 64)
+// instead of being rebuilt by complex multiplies.
 template <int N, int PTS, int R, int NS>
 struct TwiddleLds {
     static constexpr int NB = PTS / R;
@@ -180,7 +219,7 @@ struct TwiddleLds {
     const float2* tab;
     __device__ __forceinline__ static void fill(float2* tab, int tid, int nthreads) {
         for (int i = tid; i < ENTRIES; i += nthreads) {
-            const int m = i / (R - 1), r = i % (R - 1) + 1;
+            const int r = i / NS + 1, m = i % NS;
             double sn, cs;
             sincospi(-2.0 * (double)(m * r) / (double)(NS * R), &sn, &cs);
             tab[i] = make_float2((float)cs, (float)sn);
@@ -190,9 +229,10 @@ struct TwiddleLds {
         constexpr int NT = N / PTS;
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-            const float2* e = tab + ((t + q * NT) % NS) * (R - 1);
+            const float2* e = tab + (t + q * NT) % NS;
 #pragma unroll
-            for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], e[r - 1]);
+            for (int r = 1; r < R; ++r)
+                v[q * R + r] = cmul(v[q * R + r], *static_cast<const float2*>(__builtin_assume_aligned(e + (r - 1) * NS, 8)));
         }
     }
 };

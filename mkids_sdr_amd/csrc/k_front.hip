@@ -212,7 +212,9 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         for (int r = 0; r < PTS; ++r) {
             const int p = t + r * NT;
             const int hi = p / M, off = p % M;
-            const uint2 hp = hl[p];
+            // one 8-byte LDS read (a uint2 load is split into two 4-byte halves)
+            const uint64_t h64 = reinterpret_cast<const uint64_t*>(hl)[p];
+            const uint2 hp = make_uint2((uint32_t)h64, (uint32_t)(h64 >> 32));
             uint32_t w[T];
 #pragma unroll
             for (int tau = 0; tau < T; ++tau) {
@@ -275,11 +277,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
             const float2* yf = fbuf + f * G::LDSF + yoff;
             float2 X = yf[0];
 #pragma unroll
-            for (int r = 1; r < RL; ++r) {
-                const float2 yv = yf[r * NSL / 16 * 17];
-                X.x = fmaf(tl[r - 1].x, yv.x, fmaf(-tl[r - 1].y, yv.y, X.x));
-                X.y = fmaf(tl[r - 1].x, yv.y, fmaf(tl[r - 1].y, yv.x, X.y));
-            }
+            for (int r = 1; r < RL; ++r) X = cmac(X, tl[r - 1], yf[r * NSL / 16 * 17]);
             const float2 z = cmul(X, lov[f]);
 #ifdef MKID_XP_STAMPS
             if (f == 0) {

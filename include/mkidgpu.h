@@ -218,6 +218,20 @@ int mkid_make_template(mkid_ctx* ctx, const float* d_I, const float* d_Q, int64_
 int mkid_optimal_filter(mkid_ctx* ctx, const double* d_template, const double* d_noise, int32_t pre,
                         int32_t ncoeff, double* d_coeff);
 
+/* Per-packet optimal-filter pulse height, fp32 (BASELINE config 5): the filter above (or any
+ * per-channel FIR) applied to the phase stream at each photon packet,
+ *     h = sum_{i < ncoeff} coeff[ch][i] * phase[ts - pre + i][ch]     (phase in rad)
+ * the estimate the reference's PulseAnalysis.coeff was meant for (pulses.py:44-51, 398).
+ * mkid_set_pulse_filter: host coeff [nch = C][ncoeff] fp32, 1 <= ncoeff <= 4096, 0 <= pre.
+ * mkid_pulse_heights: d_phase holds the device phase rows of global phase indices
+ * j0 .. j0 + rows - 1 ([rows][C], e.g. the d_phase of one mkid_process_device call; j0 = the
+ * number of phase rows processed before it since the last reset); d_events n wide packets;
+ * d_heights n floats, NaN where the window is not inside the rows. Asynchronous on the context
+ * stream; device pointers only. */
+int mkid_set_pulse_filter(mkid_ctx* ctx, const float* coeff, int32_t nch, int32_t ncoeff, int32_t pre);
+int mkid_pulse_heights(mkid_ctx* ctx, const float* d_phase, int64_t rows, int64_t j0,
+                       const uint64_t* d_events, int64_t n, float* d_heights);
+
 /* Kernel timing with HIP events on the context stream (for bench roofline numbers). */
 #define MKID_K_CHANNELIZE 0
 #define MKID_K_FIR_PHASE 1

@@ -97,6 +97,8 @@ _SIGS = {
     'mkid_replay_trigger': [P, P, I64, I64, I32, P, P, I32, P],
     'mkid_make_template': [P, P, P, I64, P, P, P],
     'mkid_optimal_filter': [P, P, P, I32, I32, P],
+    'mkid_set_pulse_filter': [P, P, I32, I32, I32],
+    'mkid_pulse_heights': [P, P, I64, I64, P, I64, P],
     'mkid_synth_adc': [P, P, I64, I64, P, P, P, I64, ctypes.c_float, ctypes.c_float, I32,
                        ctypes.c_float, ctypes.c_uint32],
 }

@@ -178,6 +178,30 @@ class Channelizer:
                                               ctypes.byref(rc), _ptr(d_hits), int(cap), _ptr(d_counts)))
         return d_hits, d_counts
 
+    # ---- per-packet optimal-filter pulse height (BASELINE config 5) -----------------------------
+    def set_pulse_filter(self, coeff, pre):
+        """coeff: float [C][ncoeff] (one filter per channel, e.g. template.optimal_filter's weights
+        tiled); the height of a packet stamped ts is sum_i coeff[ch][i] phase[ts - pre + i][ch]."""
+        cf = np.ascontiguousarray(coeff, np.float32).reshape(self.C, -1)
+        self._chk(self._L.mkid_set_pulse_filter(self._h, _ptr(cf), cf.shape[0], cf.shape[1], int(pre)))
+
+    def pulse_heights_device(self, d_phase, rows, j0, d_events, n, d_heights):
+        """Device pointers; asynchronous on the context stream (include/mkidgpu.h)."""
+        self._chk(self._L.mkid_pulse_heights(self._h, _ptr(d_phase), int(rows), int(j0), _ptr(d_events),
+                                             int(n), _ptr(d_heights)))
+
+    def pulse_heights(self, phase, events, j0=0):
+        """Host convenience: phase float32 [rows][C] (rad) of global rows j0.., events uint64 [n]
+        -> float32 heights [n] (NaN where the window leaves the rows)."""
+        import torch
+        ph = torch.from_numpy(np.ascontiguousarray(phase, np.float32)).cuda()
+        ev = torch.from_numpy(np.ascontiguousarray(events, np.uint64).view(np.int64)).cuda()
+        out = torch.empty(ev.numel(), dtype=torch.float32, device='cuda')
+        torch.cuda.synchronize()  # the uploads run on torch's stream, the kernel on the context's
+        self.pulse_heights_device(ph, ph.shape[0], j0, ev, ev.numel(), out)
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
     # ---- timing ------------------------------------------------------------------------------
     def set_timing(self, on):
         self._chk(self._L.mkid_set_timing(self._h, 1 if on else 0))

@@ -1,0 +1,47 @@
+// Per-packet optimal-filter pulse height (BASELINE config 5: "per-channel optimal-filter
+// pulse-height estimation (fp32)"). The reference computes the pulse template and noise PSD
+// (MakeTemplate, pulses.py:239-427) but stubs the filter (pulses.py:398, PulseAnalysis.coeff
+// Float32Col(100)); mkid_optimal_filter fills the stub and this kernel applies a per-channel
+// filter of that form to the phase stream at every photon packet:
+//     h_p = sum_{i < ncoeff} coeff[ch_p][i] * phase[ts_p - pre + i][ch_p]
+// One wave per packet: lane l accumulates taps l, l + 64, ... in fp32, then a fixed-order xor
+// butterfly over the wave (deterministic). The phase rows of one packet's window are strided by
+// C floats, so each lane's read is its own cache line; the volume is small (ncoeff x 4 B per
+// packet, ~3 MB per 2^30 ADC samples at the bench's packet rate) and L2-resident right after the
+// front end wrote it.
+#include "mkid_internal.h"
+
+namespace mkid {
+
+constexpr int kHeightWaves = 4;  // packets (waves) per 256-thread workgroup
+
+__global__ __launch_bounds__(64 * kHeightWaves) void k_pulse_heights(HeightArgs a) {
+    const int64_t p = (int64_t)blockIdx.x * kHeightWaves + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= a.n) return;  // wave-uniform: the whole wave leaves
+    const uint64_t w = a.events[p];
+    const int ch = (int)((w >> MKID_PKT_CH_SHIFT) & 0xFFF);
+    const int64_t ts = (int64_t)(w & MKID_PKT_TS_MASK);
+    // global phase index of the packet: the 28-bit stamp unwrapped against the rows' origin j0
+    const int64_t jg = a.j0 + ((ts - (a.j0 & (int64_t)MKID_PKT_TS_MASK)) & (int64_t)MKID_PKT_TS_MASK);
+    const int64_t r0 = jg - a.j0 - a.pre;  // first phase row of the window
+    const bool inside = ch < a.C && r0 >= 0 && r0 + a.ncoeff <= a.rows;
+    float acc = 0.f;
+    if (inside) {
+        const float* cf = a.coeff + (size_t)ch * a.ncoeff;
+        const float* ph = a.phase + r0 * a.C + ch;
+        for (int i = lane; i < a.ncoeff; i += 64) acc = fmaf(cf[i], ph[(int64_t)i * a.C], acc);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+    if (lane == 0) a.heights[p] = inside ? acc : __builtin_nanf("");
+}
+
+hipError_t launch_pulse_heights(const HeightArgs& a, hipStream_t s) {
+    if (a.n <= 0) return hipSuccess;
+    const int64_t blocks = (a.n + kHeightWaves - 1) / kHeightWaves;
+    hipLaunchKernelGGL(k_pulse_heights, dim3((unsigned)blocks), dim3(64 * kHeightWaves), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mkid

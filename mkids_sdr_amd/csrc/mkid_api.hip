@@ -103,6 +103,8 @@ struct mkid_ctx {
     // IQ snapshot tap: low-pass output of one channel for the rows of the last call
     int32_t iq_ch = -1;
     int16_t* d_iqtap = nullptr;     // [max_chunk/N][2]
+    float* d_hcoeff = nullptr;      // [C][h_ncoeff] pulse-height filter (mkid_set_pulse_filter)
+    int32_t h_ncoeff = 0, h_pre = 0;
     int64_t iq_rows = 0;
     // host copies behind the folded LO table (d_lo = conj(LUT)/2^15 with the (-1)^(b (k+1))
     // bin-parity sign of K4 folded in: P is even, so the sign depends on k mod P only)
@@ -185,7 +187,7 @@ static void free_all(mkid_ctx* c) {
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
-                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap};
+                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -909,6 +911,33 @@ int mkid_optimal_filter(mkid_ctx* c, const double* d_template, const double* d_n
     HIPCHK(c, b.get(&work, 3 * 800));
     HIPCHK(c, launch_optimal_filter(d_template, d_noise, pre, ncoeff, d_coeff, work, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MKID_OK;
+}
+
+int mkid_set_pulse_filter(mkid_ctx* c, const float* coeff, int32_t nch, int32_t ncoeff, int32_t pre) {
+    if (!c || !coeff) return MKID_E_ARG;
+    if (nch != c->C) FAIL(c, MKID_E_ARG, "pulse filter: need one filter per channel");
+    if (ncoeff < 1 || ncoeff > 4096 || pre < 0) FAIL(c, MKID_E_ARG, "pulse filter: bad ncoeff/pre");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->d_hcoeff) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->d_hcoeff));
+        c->d_hcoeff = nullptr;
+    }
+    HIPCHK(c, dalloc(&c->d_hcoeff, (size_t)nch * ncoeff));
+    c->h_ncoeff = ncoeff;
+    c->h_pre = pre;
+    return upload(c, c->d_hcoeff, coeff, (size_t)nch * ncoeff * 4);
+}
+
+int mkid_pulse_heights(mkid_ctx* c, const float* d_phase, int64_t rows, int64_t j0, const uint64_t* d_events,
+                       int64_t n, float* d_heights) {
+    if (!c || (n > 0 && (!d_phase || !d_events || !d_heights))) return MKID_E_ARG;
+    if (rows < 0 || j0 < 0 || n < 0) FAIL(c, MKID_E_ARG, "pulse heights: negative rows/j0/n");
+    if (!c->d_hcoeff) FAIL(c, MKID_E_STATE, "pulse heights: no filter set (mkid_set_pulse_filter)");
+    HIPCHK(c, hipSetDevice(c->device));
+    HeightArgs a{d_phase, d_events, c->d_hcoeff, d_heights, rows, j0, n, c->C, c->h_ncoeff, c->h_pre};
+    HIPCHK(c, launch_pulse_heights(a, c->stream));
     return MKID_OK;
 }
 

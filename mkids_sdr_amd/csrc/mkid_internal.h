@@ -113,7 +113,17 @@ struct TrigSpecArgs {
     int32_t mode, alpha, kf, kq, base_thr, dead;
 };
 
+struct HeightArgs {
+    const float* phase;      // [rows][C] rad, global phase rows j0 .. j0 + rows - 1
+    const uint64_t* events;  // [n] wide packets
+    const float* coeff;      // [C][ncoeff] per-channel optimal filter
+    float* heights;          // [n] out (NaN: window outside the rows or unknown channel)
+    int64_t rows, j0, n;
+    int32_t C, ncoeff, pre;
+};
+
 // launchers (return hipError_t of the launch)
+hipError_t launch_pulse_heights(const HeightArgs& a, hipStream_t s);
 hipError_t launch_channelize(int N, const ChanArgs& a, hipStream_t s);
 hipError_t launch_lpf_phase(const LpfArgs& a, hipStream_t s);
 hipError_t launch_front(int N, const FrontArgs& a, hipStream_t s);

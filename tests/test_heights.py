@@ -1,0 +1,145 @@
+"""Per-packet optimal-filter pulse height (BASELINE config 5; include/mkidgpu.h
+mkid_set_pulse_filter / mkid_pulse_heights, k_heights.hip) against oracle/heights.py.
+
+CPU: the oracle against a plain double loop, including 28-bit stamp unwrapping and windows that
+leave the rows. GPU: the device heights on the device's own phase and packets, config-5 geometry
+(2048 channels, N = 4096, split front end) and a streamed 1024-channel fused case with j0 > 0;
+fp32 accumulation of <= 128 products, so the bar is relative 1e-5 of sum |coeff * phase|.
+"""
+import numpy as np
+import pytest
+
+from oracle import heights as oh
+
+
+def _pack(ch, ts):
+    return np.uint64((int(ch) << oh.CH_SHIFT) | (int(ts) & oh.TS_MASK))
+
+
+def _loop(phase, events, coeff, pre, j0):
+    out = []
+    for w in events.tolist():
+        ch, ts = w >> 52, w & oh.TS_MASK
+        jg = j0 + ((ts - (j0 & oh.TS_MASK)) & oh.TS_MASK)
+        r0 = jg - j0 - pre
+        if r0 < 0 or r0 + coeff.shape[1] > phase.shape[0]:
+            out.append(np.nan)
+            continue
+        out.append(sum(float(coeff[ch, i]) * float(phase[r0 + i, ch]) for i in range(coeff.shape[1])))
+    return np.array(out)
+
+
+@pytest.mark.parametrize('j0', [0, 1000, (1 << 28) - 7, 3 << 28])
+def test_oracle_heights_match_loop(j0):
+    rng = np.random.default_rng(5)
+    rows, C, nco, pre = 300, 8, 20, 6
+    phase = rng.normal(size=(rows, C)).astype(np.float32)
+    coeff = rng.normal(size=(C, nco))
+    ts = j0 + np.array([0, 5, 6, 50, 200, 273, 274, 299, 320])
+    ch = rng.integers(0, C, ts.size)
+    ev = np.array([_pack(c, t) for c, t in zip(ch, ts)], np.uint64)
+    ref = _loop(phase, ev, coeff, pre, j0)
+    got = oh.pulse_heights(phase, ev, coeff, pre, j0)
+    assert np.array_equal(np.isnan(ref), np.isnan(got))
+    assert np.isnan(got).sum() == 4  # windows starting before row 0 (ts 0, 5) or past the end
+    ok = ~np.isnan(ref)
+    assert np.allclose(got[ok], ref[ok], rtol=1e-12, atol=1e-12)
+
+
+def _check(phase, ev, coeff, pre, j0, got):
+    ref = oh.pulse_heights(phase, ev, coeff, pre, j0)
+    assert np.array_equal(np.isnan(ref), np.isnan(got))
+    ok = ~np.isnan(ref)
+    assert ok.sum() > 20
+    chs = (ev[ok] >> np.uint64(52)).astype(np.int64)
+    scale = np.array([np.abs(coeff[c]).sum() for c in chs]) * np.abs(phase).max()
+    assert np.all(np.abs(got[ok] - ref[ok]) <= 1e-5 * scale + 1e-6)
+
+
+@pytest.mark.gpu
+def test_heights_config5_split(gpu):
+    import signals
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 2048, 2 ** 20
+    case = signals.make_case(C, S, seed=61, pulses_per_ch=2.0)
+    quiet = signals.make_case(C, 2 ** 18, seed=61, pulses_per_ch=0)
+    r = signals.oracle_chain(quiet).process(quiet.iq)
+    thr = signals.thresholds_from_quiet(quiet, r['raw'])
+    ch = Channelizer(C, max_chunk=S)
+    try:
+        ch.set_pfb(case.pfb)
+        ch.set_bins(case.bins)
+        ch.set_dds(case.lut_i, case.lut_q)
+        ch.set_lpf(case.lpf12)
+        ch.set_fir(case.fir12)
+        ch.set_centers(case.ic, case.qc)
+        ch.set_thresholds(thr)
+        ch.set_baseline(1, 41, 82, 93623, 8192)
+        phase, ev = ch.process(case.iq)
+        rng = np.random.default_rng(62)
+        coeff = rng.normal(size=(C, 100)).astype(np.float32)
+        ch.set_pulse_filter(coeff, pre=20)
+        got = ch.pulse_heights(phase, ev)
+    finally:
+        ch.close()
+    assert ev.size > 100
+    _check(phase, ev, coeff.astype(np.float64), 20, 0, got)
+
+
+@pytest.mark.gpu
+def test_heights_streamed_fused_j0(gpu):
+    """Two device calls; heights of the second call's packets on its own phase rows (j0 = the
+    first call's rows), with a 128-tap filter (two passes per lane)."""
+    import torch
+    import signals
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 1024, 2 ** 20
+    case = signals.make_case(C, 2 * S, seed=63, pulses_per_ch=3.0)
+    ch = Channelizer(C, max_chunk=S)
+    try:
+        ch.set_pfb(case.pfb)
+        ch.set_bins(case.bins)
+        ch.set_dds(case.lut_i, case.lut_q)
+        ch.set_lpf(case.lpf12)
+        ch.set_fir(case.fir12)
+        ch.set_centers(case.ic, case.qc)
+        ch.set_thresholds(np.full(C, -1500, np.int32))
+        ch.set_baseline(1, 41, 82, 93623, 8192)
+        J = S // (2 * C)
+        x = torch.from_numpy(np.ascontiguousarray(case.iq)).cuda()
+        d_ph = torch.empty((J, C), dtype=torch.float32, device='cuda')
+        cap = J * C
+        d_ev = torch.empty(cap, dtype=torch.int64, device='cuda')
+        d_cnt = torch.zeros(2, dtype=torch.int64, device='cuda')
+        torch.cuda.synchronize()
+        ch.process_device(x[:S], S, d_ph, d_ev, cap, d_cnt)
+        ch.process_device(x[S:], S, d_ph, d_ev, cap, d_cnt)
+        rng = np.random.default_rng(64)
+        coeff = rng.normal(size=(C, 128)).astype(np.float32)
+        ch.set_pulse_filter(coeff, pre=40)
+        torch.cuda.synchronize()
+        n = int(d_cnt[0].item())
+        d_h = torch.empty(max(n, 1), dtype=torch.float32, device='cuda')
+        ch.pulse_heights_device(d_ph, J, J, d_ev, n, d_h)
+        torch.cuda.synchronize()
+        got = d_h[:n].cpu().numpy()
+        phase = d_ph.cpu().numpy()
+        ev = d_ev[:n].cpu().numpy().view(np.uint64)
+    finally:
+        ch.close()
+    assert n > 100
+    _check(phase, ev, coeff.astype(np.float64), 40, J, got)
+
+
+@pytest.mark.gpu
+def test_heights_errors(gpu):
+    from mkids_sdr_amd import _lib
+    from mkids_sdr_amd.channelizer import Channelizer
+    ch = Channelizer(64, max_chunk=2 ** 14)
+    try:
+        with pytest.raises(_lib.MkidError):
+            ch.pulse_heights(np.zeros((4, 64), np.float32), np.zeros(1, np.uint64))  # no filter yet
+        with pytest.raises(_lib.MkidError):
+            ch.set_pulse_filter(np.zeros((64, 10), np.float32), pre=-1)  # negative pre-trigger
+    finally:
+        ch.close()

@@ -176,16 +176,17 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     uint4 pre = front_load<N>(a, k_start + FPB, tid);
     __syncthreads();
 
-#if defined(MKID_PRIO) && MKID_PRIO == 1
-    if (__builtin_amdgcn_readfirstlane(tid) >= G::BT / 2) __builtin_amdgcn_s_setprio(1);
-#elif defined(MKID_PRIO) && MKID_PRIO == 2
+    // static issue priority by dispatch order (MI355X_MICROARCH.md "two waves per SIMD" item 4):
+    // the later-dispatched waves of a SIMD lose every age-based arbitration and reach each barrier
+    // last; raising them once before the loop trims that skew (-0.7..-1 % k_front, same-box A/B
+    // profiles/r01_v28_kbench_prio.json)
     {
         const int w = __builtin_amdgcn_readfirstlane(tid) / 64, nw = G::BT / 64;
-        if (w >= nw / 4 && w < nw / 2) __builtin_amdgcn_s_setprio(1);
-        if (w >= nw / 2 && w < 3 * nw / 4) __builtin_amdgcn_s_setprio(2);
-        if (w >= 3 * nw / 4) __builtin_amdgcn_s_setprio(3);
+        const int pr = nw >= 4 ? w * 4 / nw : 0;  // 0..3 by quarter of the workgroup
+        if (pr == 1) __builtin_amdgcn_s_setprio(1);
+        if (pr == 2) __builtin_amdgcn_s_setprio(2);
+        if (pr == 3) __builtin_amdgcn_s_setprio(3);
     }
-#endif
     float2 acc[13];
 #pragma unroll
     for (int m = 0; m < 13; ++m) acc[m] = make_float2(0.f, 0.f);
@@ -212,11 +213,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
         // LO rows of this iteration's frames (latency hidden behind the FFT)
         float2 lov[FPB];
 #pragma unroll
-#ifdef MKID_XP_NOLO
-        for (int f = 0; f < FPB; ++f) lov[f] = make_float2(1.f + f * 1e-3f, 0.5f);  // what-if: no LO loads
-#else
         for (int f = 0; f < FPB; ++f) lov[f] = (a.lo + ((lrow + f) & (a.P - 1)) * C)[c];
-#endif
 
         // ---- PFB of frame kb + slot from the LDS ring ----
         int sb = rb + slot;

@@ -56,26 +56,23 @@ def _check(phase, ev, coeff, pre, j0, got):
     assert np.all(np.abs(got[ok] - ref[ok]) <= 1e-5 * scale + 1e-6)
 
 
+def _noise_iq(S, seed):
+    """Random int16 I/Q: the chain turns it into noise-like phase that crosses the thresholds
+    often, which is all the pulse-height check needs (it runs on the device's own phase and
+    packets; the chain itself is checked in test_gpu_parity.py)."""
+    rng = np.random.default_rng(seed)
+    return rng.integers(-12000, 12000, size=(S, 2), dtype=np.int16)
+
+
 @pytest.mark.gpu
 def test_heights_config5_split(gpu):
-    import signals
     from mkids_sdr_amd.channelizer import Channelizer
-    C, S = 2048, 2 ** 20
-    case = signals.make_case(C, S, seed=61, pulses_per_ch=2.0)
-    quiet = signals.make_case(C, 2 ** 18, seed=61, pulses_per_ch=0)
-    r = signals.oracle_chain(quiet).process(quiet.iq)
-    thr = signals.thresholds_from_quiet(quiet, r['raw'])
+    C, S = 2048, 2 ** 20                       # config 5 geometry: N = 4096, split front end
     ch = Channelizer(C, max_chunk=S)
     try:
-        ch.set_pfb(case.pfb)
-        ch.set_bins(case.bins)
-        ch.set_dds(case.lut_i, case.lut_q)
-        ch.set_lpf(case.lpf12)
-        ch.set_fir(case.fir12)
-        ch.set_centers(case.ic, case.qc)
-        ch.set_thresholds(thr)
-        ch.set_baseline(1, 41, 82, 93623, 8192)
-        phase, ev = ch.process(case.iq)
+        ch.set_fir(np.tile(np.arange(26, dtype=np.int16) * 40 - 500, (C, 1)))
+        ch.set_thresholds(np.full(C, -200, np.int32))
+        phase, ev = ch.process(_noise_iq(S, 61))
         rng = np.random.default_rng(62)
         coeff = rng.normal(size=(C, 100)).astype(np.float32)
         ch.set_pulse_filter(coeff, pre=20)
@@ -88,25 +85,17 @@ def test_heights_config5_split(gpu):
 
 @pytest.mark.gpu
 def test_heights_streamed_fused_j0(gpu):
-    """Two device calls; heights of the second call's packets on its own phase rows (j0 = the
-    first call's rows), with a 128-tap filter (two passes per lane)."""
+    """Two device calls through the fused front end; heights of the second call's packets on its
+    own phase rows (j0 = the first call's rows), with a 128-tap filter (two passes per lane)."""
     import torch
-    import signals
     from mkids_sdr_amd.channelizer import Channelizer
     C, S = 1024, 2 ** 20
-    case = signals.make_case(C, 2 * S, seed=63, pulses_per_ch=3.0)
     ch = Channelizer(C, max_chunk=S)
     try:
-        ch.set_pfb(case.pfb)
-        ch.set_bins(case.bins)
-        ch.set_dds(case.lut_i, case.lut_q)
-        ch.set_lpf(case.lpf12)
-        ch.set_fir(case.fir12)
-        ch.set_centers(case.ic, case.qc)
-        ch.set_thresholds(np.full(C, -1500, np.int32))
-        ch.set_baseline(1, 41, 82, 93623, 8192)
+        ch.set_fir(np.tile(np.arange(26, dtype=np.int16) * 40 - 500, (C, 1)))
+        ch.set_thresholds(np.full(C, -200, np.int32))
         J = S // (2 * C)
-        x = torch.from_numpy(np.ascontiguousarray(case.iq)).cuda()
+        x = torch.from_numpy(_noise_iq(2 * S, 63)).cuda()
         d_ph = torch.empty((J, C), dtype=torch.float32, device='cuda')
         cap = J * C
         d_ev = torch.empty(cap, dtype=torch.int64, device='cuda')

@@ -1,18 +1,31 @@
 #!/usr/bin/env python3
-"""Benchmark: ADC MSample/s per GPU through the full MKID chain at 1024 channels (BASELINE.json
-configs[2]: "1024-ch full chain incl. matched-filter pulse trigger, 1 MI355X"), one feedline per
-GPU, photon-packet lists gathered to rank 0 over RCCL (configs[3] when N > 1).
+"""Benchmark: ADC MSample/s per GPU through the full MKID chain (BASELINE.json metric "ADC
+MSample/s/GPU at 1024 ch; achieved HBM GB/s vs roofline"), one feedline per GPU, photon-packet
+lists gathered to rank 0 over RCCL when N > 1 (configs[3]).
 
-A step = one pass of the hot path over one batch of 2^30 synthetic int16 I/Q samples resident in
-HBM (4 GiB): PFB+FFT+DDC -> IQ low-pass/2 + phase (materialised, fp32) -> matched filter +
-baseline + trigger -> packets; then the packet gather. Prints ONE JSON line on rank 0.
+A step = one pass of the hot path over one batch of synthetic int16 I/Q samples resident in HBM:
+PFB+FFT+DDC -> IQ low-pass/2 + phase (materialised, fp32) -> matched filter + baseline + trigger
+-> packets (-> per-packet fp32 optimal-filter pulse heights for config 5); then the packet gather.
+Prints ONE JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,3,5}] [--baseline {ema,svf}]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Configs (BASELINE.json `configs`; the default is configs[2], the one the
+metric is quoted on):
+  2  256 ch, N = 512, fs = 550 MS/s, 2^28 samples per step
+  3  1024 ch, N = 2048, fs = 550 MS/s, 2^30 samples per step (default)
+  5  2048 ch, N = 4096, fs = 2 GS/s, 2^30 samples per step, pulse heights in the step
+
+Roofline: algorithmic bytes are 4 B of int16 I/Q read + 2 B of fp32 phase
+written per ADC sample for the chain; a kernel's own share of those bytes over its HIP-event
+launch time (on the stream it runs on) is `roofline.achieved`. Intermediate traffic (the
+Fix16_13 raw phase, the staged baseband of the split front end) is overhead, reported as such.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -24,7 +37,15 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFLOPS = 157.3        # MI355X_MICROARCH.md chip table (vector FP32)
 ALG_BYTES_PER_SAMPLE = 6.0      # 4 B int16 I/Q in + 2 B fp32 phase out
-CHAN_FLOPS_PER_SAMPLE = None    # filled from the FFT size below
+
+CONFIGS = {
+    2: dict(channels=256, fs=550e6, log2=28, heights=False,
+            name='config2: 256-ch PFB+FFT + DDC + phase (+ trigger), fs=550 MS/s'),
+    3: dict(channels=1024, fs=550e6, log2=30, heights=False,
+            name='config3: 1024-ch full chain incl. matched-filter trigger, fs=550 MS/s'),
+    5: dict(channels=2048, fs=2e9, log2=30, heights=True,
+            name='config5: 2048-ch full chain + per-packet fp32 optimal-filter pulse heights, fs=2 GS/s'),
+}
 
 
 def parse():
@@ -32,14 +53,16 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=10)
     p.add_argument('--warmup', type=int, default=2)
-    p.add_argument('--channels', type=int, default=1024)
-    p.add_argument('--fs', type=float, default=550e6)
-    p.add_argument('--log2-samples', type=int, default=30)
+    p.add_argument('--config', type=int, default=3, choices=sorted(CONFIGS))
+    p.add_argument('--baseline', default='ema', choices=['ema', 'svf'])
+    p.add_argument('--log2-samples', type=int, default=None, help='override the config sample count')
     p.add_argument('--pulse-rate', type=float, default=1.0 / 2048,
                    help='Poisson pulses per phase sample per channel')
-    p.add_argument('--cpu-samples-log2', type=int, default=26)
+    p.add_argument('--cpu-samples-log2', type=int, default=26, help='one-core CPU baseline sample')
+    p.add_argument('--cpu-all-samples-log2', type=int, default=28, help='all-core CPU baseline sample')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-phase', action='store_true', help='do not materialise the phase stream')
+    p.add_argument('--copy-mib', type=int, default=2048, help='stream-copy probe size (MiB)')
     return p.parse_args()
 
 
@@ -52,7 +75,7 @@ def setup_feedline(C, fs, seed):
     upb = lut.LUT_LEN // N
     rng = np.random.default_rng(seed)
     bins = rng.permutation(np.arange(1, N))[:C]
-    m = rng.integers(-(upb // 4), upb // 4 + 1, C)
+    m = rng.integers(-(upb // 4), upb // 4 + 1, C) if upb >= 4 else np.zeros(C, int)
     f_base = 4.0e9
     f_rf = [f_base + float((int(b) * upb + int(k)) * res) for b, k in zip(bins, m)]
     f_rf = [f - fs if f - f_base >= fs / 2 else f for f in f_rf]     # keep within +-fs/2 of LO
@@ -65,7 +88,7 @@ def setup_feedline(C, fs, seed):
                 f_rf=f_rf, f_base=f_base)
 
 
-def make_pulses(C, n_samples, N, rate, rng, tau_fall=65.0, window_phase=390):
+def make_pulses(C, n_samples, N, rate, rng):
     J = n_samples // N
     starts, tones, amps = [], [], []
     for ch in range(C):
@@ -77,6 +100,42 @@ def make_pulses(C, n_samples, N, rate, rng, tau_fall=65.0, window_phase=390):
     s = np.concatenate(starts)
     o = np.argsort(s, kind='stable')
     return s[o], np.concatenate(tones)[o], np.concatenate(amps)[o]
+
+
+def detector_score(ev, j_last, ps, pt, N, early=2, late=60, isolation=400):
+    """Packets of the last step against the injected pulses (start sample ps, channel pt): a packet
+    of channel c at row r matches a pulse of c starting at row p when p - early <= r <= p + late.
+    Returns the fraction of isolated pulses (no other pulse of the channel within `isolation`
+    rows) with exactly one packet, and the packets matching no pulse."""
+    ev = np.asarray(ev, np.uint64)
+    ch = ((ev >> np.uint64(52)) & np.uint64(0xFFF)).astype(np.int64)
+    row = ((ev & np.uint64((1 << 28) - 1)).astype(np.int64) - j_last) % (1 << 28)
+    prow = np.asarray(ps, np.int64) // N
+    pch = np.asarray(pt, np.int64)
+    key = pch * (1 << 40) + prow
+    o = np.argsort(key)
+    key, pch, prow = key[o], pch[o], prow[o]
+    k = np.searchsorted(key, ch * (1 << 40) + row + early, side='right') - 1
+    ok = (k >= 0) & (pch[np.maximum(k, 0)] == ch) & (row >= prow[np.maximum(k, 0)] - early) & \
+        (row <= prow[np.maximum(k, 0)] + late)
+    nhit = np.bincount(k[ok], minlength=len(key))
+    same_prev = np.r_[False, pch[1:] == pch[:-1]] & (np.r_[0, np.diff(prow)] < isolation)
+    same_next = np.r_[pch[1:] == pch[:-1], False] & (np.r_[np.diff(prow), 0] < isolation)
+    iso = ~(same_prev | same_next)
+    return dict(isolated=int(iso.sum()), exactly_one_frac=round(float((nhit[iso] == 1).mean()), 4) if iso.any() else None,
+                missed=int((nhit[iso] == 0).sum()), multi=int((nhit[iso] > 1).sum()),
+                unmatched_packets=int((~ok).sum()), packets=int(len(ev)))
+
+
+def pulse_filter(C, npre=20, ncoeff=100, tau_fall=65.0):
+    """Config 5 per-channel filter: the matched (template) filter of the injected pulse shape
+    -(1 - e^{-t/0.1}) e^{-t/65} (pulses.py:470-472) over ncoeff phase rows starting npre rows
+    before the packet's peak stamp, normalised to unit response to a unit-amplitude pulse; one
+    row per channel (mkid_set_pulse_filter). Returns (coeff [C][ncoeff], pre)."""
+    t = np.arange(ncoeff, dtype=np.float64) - npre
+    tpl = np.where(t >= 0, -(1 - np.exp(-np.maximum(t, 0) / 0.1)) * np.exp(-np.maximum(t, 0) / tau_fall), 0.0)
+    g = tpl / np.dot(tpl, tpl)
+    return np.tile(g.astype(np.float32), (C, 1)), npre
 
 
 def main():
@@ -97,15 +156,18 @@ def main():
     from mkids_sdr_amd.channelizer import Channelizer
     from mkids_sdr_amd import codecs
 
-    C = args.channels
+    cf = CONFIGS[args.config]
+    C = cf['channels']
     N = 2 * C
-    S = 1 << args.log2_samples
+    log2 = cf['log2'] if args.log2_samples is None else args.log2_samples
+    S = 1 << log2
     J = S // N
-    fs = args.fs
+    fs = cf['fs']
     feed = setup_feedline(C, fs, 1000 + rank)
     mf = codecs.fir_quantise(np.loadtxt(os.path.join(ROOT, 'tests', 'golden', 'fir', 'matched_30us.txt')))
     lpf = codecs.fir_quantise(np.loadtxt(os.path.join(ROOT, 'tests', 'golden', 'fir',
                                                       'BlackmanFilter_250kHz.txt')))
+    base_mode = _lib.BASE_SVF if args.baseline == 'svf' else _lib.BASE_EMA
 
     ch = Channelizer(C, device=local, max_chunk=S, dead_time=32, sample_rate=fs)
     stream = torch.cuda.current_stream(dev)
@@ -114,7 +176,7 @@ def main():
     ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
     ch.set_lpf(lpf)
     ch.set_fir(np.tile(mf, (C, 1)))
-    ch.set_baseline(_lib.BASE_EMA, 41, 82, 93623, 8192)
+    ch.set_baseline(base_mode, 41, 82, 93623, 8192)
 
     # ---- synthetic input resident in HBM ----
     rng = np.random.default_rng(42 + rank)
@@ -135,7 +197,9 @@ def main():
     # ---- loop calibration + thresholds the reference way, on a pulse-free stream:
     #      rotateLoopsReady (ROACH_Setup.py:645-667: DDS phase = arctan2 of the on-resonance avg
     #      IQ, so every channel's phase sits near 0), then loadThresholds (ROACH_Pulses.py:211-299)
-    quiet_n = 1 << 24
+    #      on snapshots of the RUNNING stream: the quiet block is processed twice and the second
+    #      pass (filters settled, no start-up transient) is the snapshot
+    quiet_n = min(1 << 24, S)
     q = torch.empty(quiet_n * 2, dtype=torch.int16, device=dev)
     ch.synth_adc(q, quiet_n, 0, base, d_tones, d_pul, 0, 0.1 * N, 65.0 * N, 390 * N, sigma, 7 + rank)
     qphase = torch.empty((quiet_n // N) * C, dtype=torch.float32, device=dev)
@@ -151,6 +215,7 @@ def main():
     ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
     ch.reset()
     ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
+    ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
     torch.cuda.synchronize(dev)
     raw_q = torch.clamp(torch.round(qphase * 8192), -25736, 25736).view(-1, C).cpu().numpy().astype(np.int64)
     thr = codecs.thresholds_from_phase_block(raw_q)
@@ -159,11 +224,24 @@ def main():
     del q, qphase
 
     phase = None if args.no_phase else torch.empty(J * C, dtype=torch.float32, device=dev)
+    heights = None
+    if cf['heights']:
+        if phase is None:
+            raise SystemExit('config 5 needs the phase stream (pulse heights read it)')
+        coeff, pre = pulse_filter(C)
+        ch.set_pulse_filter(coeff, pre)
+        heights = torch.empty(cap, dtype=torch.float32, device=dev)
 
     from mkids_sdr_amd.feedlines import gather_packets
+    j0 = [0]
 
     def step():
         ch.process_device(x, S, phase, d_events, cap, d_counts)
+        if heights is not None:
+            # every packet of the step; the written count d_counts[1] is read on the device (no
+            # host round trip inside the step); NaN where the window leaves the step's rows
+            ch.pulse_heights_counted(phase, J, j0[0], d_events, d_counts[1:], cap, heights)
+        j0[0] += J
         if world > 1:   # photon-list gather to rank 0 (the path's one exchange step)
             gather_packets(d_events, int(d_counts[1].item()), dst=0)
 
@@ -188,34 +266,61 @@ def main():
     timing = ch.timing()
     counts = d_counts.cpu().numpy()
     ev_last = int(counts[0])
+    det = None
+    if rank == 0:
+        det = detector_score(d_events[:int(counts[1])].cpu().numpy().view(np.uint64),
+                             (args.warmup + args.steps - 1) * J, ps, pt, N)
     reruns = ch.trigger_reruns()
+    ch.set_timing(False)
 
     if rank == 0:
+        # measured HBM roof in the same run: stream copy of copy_mib MiB, HIP-event timed
+        nb = args.copy_mib << 20
+        src = torch.empty(nb // 4, dtype=torch.int32, device=dev).fill_(1)
+        dst = torch.empty_like(src)
+        torch.cuda.synchronize(dev)
+        ch.set_timing(True)
+        for _ in range(6):
+            ch.stream_copy(dst, src, nb)
+        ct = ch.timing()['k_stream_copy']
+        ch.set_timing(False)
+        copy_gbps = 2.0 * nb / (ct[0] / ct[1] * 1e-3) / 1e9
+        del src, dst
+
         total = S * args.steps * world
         value = total / dt / 1e6
         ms_step = dt / args.steps * 1e3
-        kt = {k: (v[0] / max(v[1], 1)) for k, v in timing.items()}
+        kt = {k: (v[0] / max(v[1], 1)) for k, v in timing.items() if v[1] > 0}
         dom = max(kt, key=kt.get)
         n_launch = timing[dom][1] // args.steps if timing[dom][1] else 1
-        # algorithmic HBM bytes per ADC sample of each kernel (DESIGN.md "Kernels"): the fused
-        # front end reads 4 B of I/Q and writes 1 B of raw phase (+2 B of float phase)
-        alg = {'k_front': 5.0 + (0.0 if args.no_phase else 2.0),
-               'k_channelize': 4.0, 'k_lpf_phase': 1.0 + (0.0 if args.no_phase else 2.0),
-               'k_trigger': 0.0, 'k_compact': 0.0}
         per_launch_samples = S / max(n_launch, 1)
+        ph_b = 0.0 if args.no_phase else 2.0
+        # algorithmic bytes per ADC sample of each kernel's share of the chain;
+        # intermediates (raw Fix16_13 phase 1 B/sample, staged z 16 B/sample) are overhead
+        alg = {'k_front': 4.0 + ph_b, 'k_channelize': 4.0, 'k_lpf_phase': ph_b,
+               'k_trigger': 0.0, 'k_compact': 0.0, 'k_pulse_heights': 0.0}
+        overhead = {'k_front': 1.0, 'k_channelize': 8.0, 'k_lpf_phase': 8.0 + 1.0, 'k_trigger': 1.25}
         a_bytes = alg.get(dom, 0.0) * per_launch_samples
         achieved = a_bytes / (kt[dom] * 1e-3) / 1e9 if kt[dom] > 0 else 0.0
         traffic = None
         prof = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
         if os.path.exists(prof):
             try:
-                bps = json.load(open(prof)).get(dom, {}).get('hbm_bytes_per_sample')
+                rec = json.load(open(prof)).get('config%d' % args.config, {}).get(dom, {})
+                bps = rec.get('hbm_bytes_per_sample')
                 traffic = None if bps is None else round(bps * per_launch_samples)
-            except Exception:
+            except (OSError, ValueError):
                 traffic = None
+        prof_ms = None
+        kp = os.path.join(ROOT, 'profiles', 'kernel_avg_ms.json')
+        if os.path.exists(kp):
+            try:
+                prof_ms = json.load(open(kp)).get('config%d' % args.config, {}).get(dom)
+            except (OSError, ValueError):
+                prof_ms = None
         fft_flops = 5.0 * N * np.log2(N) / (N / 2)      # per input sample (hop N/2)
         flops_per_sample = 8 * 4 + fft_flops + 8 + 52 + 20 + 26
-        chain_gbps = ALG_BYTES_PER_SAMPLE * total / dt / 1e9
+        chain_gbps = (4.0 + ph_b) * total / dt / 1e9
         out = {
             'metric': 'ADC MSample/s/GPU at 1024 ch; achieved HBM GB/s vs roofline',
             'value': round(value, 1),
@@ -227,55 +332,81 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
-            'dtype': 'fp32+int16',
+            'dtype': 'int16 in, fp32 DSP, int16 Fix16_13 trigger',
             'data': 'synthetic (seeded tone comb + AWGN + Poisson photon pulses, generated in HBM)',
-            'config': {'workload': 'config3: %d-ch full chain incl. matched-filter trigger, fs=%.0f MS/s, '
-                                   '2^%d int16 I/Q samples per GPU per step' % (C, fs / 1e6, args.log2_samples),
-                       'channels': C, 'fft_len': N, 'pfb_taps': 4, 'samples_per_step_per_gpu': S,
+            'config': {'workload': '%s, 2^%d int16 I/Q samples per GPU per step' % (cf['name'], log2),
+                       'config': args.config, 'channels': C, 'fft_len': N, 'pfb_taps': 4,
+                       'fs': fs, 'samples_per_step_per_gpu': S, 'baseline': args.baseline,
                        'phase_materialised': not args.no_phase,
+                       'pulse_heights_in_step': bool(cf['heights']),
                        'parallelism': 'feedline-per-GPU x%d, RCCL packet gather' % world},
             'per_gpu_msps': round(value / world, 1),
             'packets_per_step_rank0': ev_last,
             'injected_pulses_rank0': int(len(ps)),
+            'packets_per_injected_pulse': round(ev_last / max(1, len(ps)), 4),
+            'detector': det,
             'trigger_segments_rerun': reruns,
             'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1),
                          'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
                          'frac': round(achieved / HBM_PEAK_GBPS, 4), 'traffic': traffic,
+                         'alg_bytes_per_sample': alg.get(dom, 0.0),
+                         'overhead_bytes_per_sample': overhead.get(dom, 0.0),
                          'alg_bytes_per_launch': a_bytes, 'avg_launch_ms': round(kt[dom], 4),
+                         'avg_launch_ms_rocprof': prof_ms,
+                         'stream_copy_GBps': round(copy_gbps, 1),
+                         'frac_vs_measured': round(achieved / copy_gbps, 4) if copy_gbps > 0 else None,
                          'chain_alg_GBps': round(chain_gbps, 1),
                          'chain_frac': round(chain_gbps / HBM_PEAK_GBPS, 4),
+                         'chain_frac_vs_measured': round(chain_gbps / copy_gbps, 4) if copy_gbps > 0 else None,
                          'compute_tflops_est': round(flops_per_sample * total / dt / 1e12, 2),
                          'compute_peak_tflops': FP32_PEAK_TFLOPS},
             'kernel_ms': {k: round(v, 4) for k, v in kt.items()},
         }
         if not args.no_cpu_baseline and world == 1:
-            out['cpu_baseline'] = cpu_baseline(x, C, feed, lpf, mf, thr, fs, 1 << args.cpu_samples_log2)
+            out['cpu_baseline'] = cpu_baseline(x, C, feed, lpf, mf, thr, 1 << args.cpu_samples_log2,
+                                               1 << args.cpu_all_samples_log2)
         print(json.dumps(out), flush=True)
     ch.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(x, C, feed, lpf, mf, thr, fs, n):
-    """The oracle (numpy float64 chain + C trigger, one core) on the first n samples of the same
-    GPU input (cpu_baseline.kind = 'port')."""
-    sys.path.insert(0, os.path.join(ROOT, 'tests'))
-    from oracle import chain, trigger
-    iq = x[:2 * n].view(-1, 2).cpu().numpy()
-    N = 2 * C
-    o = chain.OracleChain(C, chain.pfb_prototype(N), feed['dds']['bins'], feed['dds']['lut_i'],
-                          feed['dds']['lut_q'], lpf)
-    tr = trigger.Trigger(C, np.tile(mf, (C, 1)), thr)
-    blk = 1 << 22
-    t0 = time.perf_counter()
-    nev = 0
-    for a in range(0, n, blk):
-        r = o.process(iq[a:a + blk])
-        _, k, _ = tr.run(r['raw'])
-        nev += k
-    dt = time.perf_counter() - t0
-    return {'value': round(n / dt / 1e6, 3), 'unit': 'MSample/s', 'cores': 1, 'kind': 'port',
-            'sample': 'first 2^%d samples of the GPU input, %.1f s, %d packets' % (int(np.log2(n)), dt, nev)}
+def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall):
+    """The oracle (numpy float64 chain + C trigger) on a bounded sample of the same GPU input,
+    timed by tools/cpu_baseline.py in a child process: (i) one pinned core, (ii) all usable
+    cores chunk-parallel (cpu_baseline.kind = 'port'). `value` is the one-core rate."""
+    from mkids_sdr_amd.pfb import pfb_prototype
+    n = max(n1, nall)
+    n = min(n, x.numel() // 2)
+    tmp = '/dev/shm' if os.path.isdir('/dev/shm') else '/tmp'
+    inp = os.path.join(tmp, 'mkid_cpu_in_%d.npy' % os.getpid())
+    cfgp = os.path.join(tmp, 'mkid_cpu_cfg_%d.npz' % os.getpid())
+    try:
+        np.save(inp, x[:2 * n].view(-1, 2).cpu().numpy())
+        np.savez(cfgp, C=C, pfb=pfb_prototype(2 * C), bins=feed['dds']['bins'], lut_i=feed['dds']['lut_i'],
+                 lut_q=feed['dds']['lut_q'], lpf=lpf, fir=np.tile(mf, (C, 1)), thr=np.asarray(thr))
+        env = dict(os.environ)
+        for k in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
+            env[k] = '1'
+        r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--input', inp,
+                            '--cfg', cfgp, '--one-core-samples', str(min(n1, n)),
+                            '--all-core-samples', str(min(nall, n))],
+                           env=env, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            return {'value': None, 'unit': 'MSample/s', 'cores': 1, 'kind': 'port',
+                    'sample': 'cpu baseline failed: %s' % r.stderr[-400:]}
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        for p in (inp, cfgp):
+            try:
+                os.remove(p)
+            except OSError:
+                pass
+    one, allc = res['one_core'], res['all_cores']
+    return {'value': one['value'], 'unit': 'MSample/s', 'cores': 1, 'kind': 'port',
+            'sample': one['sample'] + ' (1 pinned core, OMP/BLAS threads 1)',
+            'all_cores': allc, 'c1_cpu_only': res['c1'], 'cpu_model': res['cpu_model'],
+            'os_cpu_count': res['os_cpu_count'], 'sched_affinity': res['sched_affinity']}
 
 
 if __name__ == '__main__':

@@ -137,11 +137,21 @@ int mkid_reset_stream(mkid_ctx* ctx);
 int mkid_process(mkid_ctx* ctx, const int16_t* iq, int64_t nsamples, float* phase_out,
                  uint64_t* events_out, int64_t cap, int64_t* nevents);
 
-/* Same with device pointers, asynchronous on the context stream. d_counts is a device int64[2]:
- * [0] = packets produced (may exceed cap), [1] = packets written. d_phase may be NULL (the phase
- * stream is then not materialised; the trigger still runs on the Fix16_13 phase). */
+/* Same with device pointers, asynchronous on the context stream; nsamples <= cfg.max_chunk (the
+ * workspace size; MKID_E_ARG otherwise). d_counts is a device int64[2]: [0] = packets produced
+ * (may exceed cap), [1] = packets written, channel-major and time-ascending within a channel over
+ * the whole call. d_phase may be NULL (the phase stream is then not materialised; the trigger
+ * still runs on the Fix16_13 phase). */
 int mkid_process_device(mkid_ctx* ctx, const int16_t* d_iq, int64_t nsamples, float* d_phase,
                         uint64_t* d_events, int64_t cap, int64_t* d_counts /* [2] */);
+
+/* K7 + K8 alone on caller-supplied Fix16_13 phase rows [rows][C] int16 (device pointer, e.g. a
+ * snapshot uploaded by the caller: the reference runs its trigger on snapshots too,
+ * ROACH_Pulses.py:211-354, 614-727): matched filter, baseline, trigger, packets, with the
+ * context's carried trigger state and phase-sample counter (advanced by rows). rows <=
+ * max_chunk/N. d_counts / packet order as mkid_process_device. Asynchronous on the context stream. */
+int mkid_trigger_phase(mkid_ctx* ctx, const int16_t* d_raw, int64_t rows, uint64_t* d_events,
+                       int64_t cap, int64_t* d_counts /* [2] */);
 
 /* Fixed-point phase of the last processed call, [J][C] int16 Fix16_13 (the trigger's input),
  * device pointer valid until the next process call. Replaces the snapPhase_bram source
@@ -231,6 +241,11 @@ int mkid_optimal_filter(mkid_ctx* ctx, const double* d_template, const double* d
 int mkid_set_pulse_filter(mkid_ctx* ctx, const float* coeff, int32_t nch, int32_t ncoeff, int32_t pre);
 int mkid_pulse_heights(mkid_ctx* ctx, const float* d_phase, int64_t rows, int64_t j0,
                        const uint64_t* d_events, int64_t n, float* d_heights);
+/* The same with the packet count read on the device: min(*d_count, cap) packets, e.g. d_count =
+ * &d_counts[1] of the mkid_process_device call that wrote d_events (no host round trip). */
+int mkid_pulse_heights_counted(mkid_ctx* ctx, const float* d_phase, int64_t rows, int64_t j0,
+                               const uint64_t* d_events, const int64_t* d_count, int64_t cap,
+                               float* d_heights);
 
 /* Kernel timing with HIP events on the context stream (for bench roofline numbers). */
 #define MKID_K_CHANNELIZE 0
@@ -238,10 +253,17 @@ int mkid_pulse_heights(mkid_ctx* ctx, const float* d_phase, int64_t rows, int64_
 #define MKID_K_TRIGGER 2
 #define MKID_K_COMPACT 3
 #define MKID_K_FRONT 4        /* fused K1-K6 (replaces CHANNELIZE + FIR_PHASE when used) */
-#define MKID_K_COUNT 5
+#define MKID_K_COPY 5         /* mkid_stream_copy (measured HBM roof)                     */
+#define MKID_K_HEIGHTS 6      /* mkid_pulse_heights                                       */
+#define MKID_K_COUNT 7
 int mkid_set_timing(mkid_ctx* ctx, int32_t enable);
 int mkid_get_timing(mkid_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches);
 const char* mkid_kernel_name(int32_t kernel);
+
+/* Diagnostic, not on the hot path: HBM stream copy d_dst = d_src (bytes a multiple of 16, both
+ * 16-byte aligned), device pointers, asynchronous on the context stream, timed as MKID_K_COPY.
+ * bench.py reads the chip's achievable bandwidth from it in the same run. */
+int mkid_stream_copy(mkid_ctx* ctx, void* d_dst, const void* d_src, int64_t bytes);
 
 /* Synthetic ADC source for tests/bench (device; NOT part of the hot path):
  *   out[n] = base[(n0+n) mod 2^16] + AWGN(sigma) + sum_p amp_c e^{i theta_c(t)} (e^{i delta_p(t)} - 1)

@@ -18,7 +18,7 @@ MKID_E_OVERFLOW = -4
 MKID_E_NODEV = -5
 
 BASE_NONE, BASE_EMA, BASE_SVF = 0, 1, 2
-K_CHANNELIZE, K_FIR_PHASE, K_TRIGGER, K_COMPACT, K_FRONT, K_COUNT = 0, 1, 2, 3, 4, 5
+K_CHANNELIZE, K_FIR_PHASE, K_TRIGGER, K_COMPACT, K_FRONT, K_COPY, K_HEIGHTS, K_COUNT = 0, 1, 2, 3, 4, 5, 6, 7
 FRONT_AUTO, FRONT_SPLIT = 0, 1
 
 PKT_CH_SHIFT, PKT_PEAK_SHIFT, PKT_BASE_SHIFT = 52, 40, 28
@@ -85,6 +85,7 @@ _SIGS = {
     'mkid_reset_stream': [P],
     'mkid_process': [P, P, I64, P, P, I64, P],
     'mkid_process_device': [P, P, I64, P, P, I64, P],
+    'mkid_trigger_phase': [P, P, I64, P, I64, P],
     'mkid_last_raw_phase': [P, P, P],
     'mkid_read_raw_phase': [P, P, I64, P],
     'mkid_set_iq_tap': [P, I32],
@@ -99,6 +100,8 @@ _SIGS = {
     'mkid_optimal_filter': [P, P, P, I32, I32, P],
     'mkid_set_pulse_filter': [P, P, I32, I32, I32],
     'mkid_pulse_heights': [P, P, I64, I64, P, I64, P],
+    'mkid_pulse_heights_counted': [P, P, I64, I64, P, P, I64, P],
+    'mkid_stream_copy': [P, P, P, I64],
     'mkid_synth_adc': [P, P, I64, I64, P, P, P, I64, ctypes.c_float, ctypes.c_float, I32,
                        ctypes.c_float, ctypes.c_uint32],
 }

@@ -41,12 +41,19 @@ class Channelizer:
         _lib.check(self._L.mkid_create(ctypes.byref(cfg), int(device), ctypes.byref(h)))
         self._h = h
         self.cfg = cfg
+        self.device = int(device)
         self.C = cfg.n_channels
         self.N = cfg.fft_len
         self.P = cfg.dds_entries
         self.set_pfb(pfb_prototype(self.N, cfg.pfb_taps))
 
     # ---- lifecycle -------------------------------------------------------------------------
+    def torch_device(self):
+        """The torch device of this context's GPU (allocations for it go there, not to the
+        current device)."""
+        import torch
+        return torch.device('cuda', self.device)
+
     def close(self):
         if getattr(self, '_h', None):
             self._L.mkid_destroy(self._h)
@@ -124,6 +131,28 @@ class Channelizer:
         self._chk(self._L.mkid_process_device(self._h, _ptr(d_iq), int(nsamples), _ptr(d_phase),
                                               _ptr(d_events), int(cap), _ptr(d_counts)))
 
+    def trigger_phase_device(self, d_raw, rows, d_events, cap, d_counts):
+        """K7 + K8 on device Fix16_13 phase rows [rows][C] (mkid_trigger_phase)."""
+        self._chk(self._L.mkid_trigger_phase(self._h, _ptr(d_raw), int(rows), _ptr(d_events), int(cap),
+                                             _ptr(d_counts)))
+
+    def trigger_phase(self, raw):
+        """Host convenience: raw int16 [rows][C] -> packets (uint64, channel-major)."""
+        import torch
+        dev = self.torch_device()
+        r = np.ascontiguousarray(raw, np.int16).reshape(-1, self.C)
+        d_raw = torch.from_numpy(r).to(dev)
+        cap = r.shape[0] * self.C // 2 + 64
+        d_ev = torch.empty(cap, dtype=torch.int64, device=dev)
+        d_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
+        self.trigger_phase_device(d_raw, r.shape[0], d_ev, cap, d_cnt)
+        torch.cuda.synchronize(dev)
+        n = d_cnt.cpu().numpy()
+        if n[0] > n[1]:
+            raise _lib.MkidError(_lib.MKID_E_OVERFLOW, 'trigger_phase: packets dropped')
+        return d_ev[:int(n[1])].cpu().numpy().view(np.uint64).copy()
+
     def raw_phase_ptr(self):
         p = ctypes.c_void_p()
         n = ctypes.c_int64()
@@ -169,9 +198,9 @@ class Channelizer:
         (hits [nch, cap] int32, counts [nch] int32) tensors (allocated when not given)."""
         import torch
         if d_hits is None:
-            d_hits = torch.full((nch, cap), -1, dtype=torch.int32, device='cuda')
+            d_hits = torch.full((nch, cap), -1, dtype=torch.int32, device=self.torch_device())
         if d_counts is None:
-            d_counts = torch.zeros(nch, dtype=torch.int32, device='cuda')
+            d_counts = torch.zeros(nch, dtype=torch.int32, device=self.torch_device())
         rc = _lib.ReplayCfg(int(mode), int(length), int(start), int(need), int(skip),
                             1 if wrap_negative else 0, float(threshold_deg))
         self._chk(self._L.mkid_replay_trigger(self._h, _ptr(d_raw), int(n), int(ld), int(nch),
@@ -190,16 +219,23 @@ class Channelizer:
         self._chk(self._L.mkid_pulse_heights(self._h, _ptr(d_phase), int(rows), int(j0), _ptr(d_events),
                                              int(n), _ptr(d_heights)))
 
+    def pulse_heights_counted(self, d_phase, rows, j0, d_events, d_count, cap, d_heights):
+        """As pulse_heights_device with the packet count read on the device (d_count: an int64
+        device pointer/tensor, e.g. the d_counts[1:] of the process call)."""
+        self._chk(self._L.mkid_pulse_heights_counted(self._h, _ptr(d_phase), int(rows), int(j0), _ptr(d_events),
+                                                     _ptr(d_count), int(cap), _ptr(d_heights)))
+
     def pulse_heights(self, phase, events, j0=0):
         """Host convenience: phase float32 [rows][C] (rad) of global rows j0.., events uint64 [n]
         -> float32 heights [n] (NaN where the window leaves the rows)."""
         import torch
-        ph = torch.from_numpy(np.ascontiguousarray(phase, np.float32)).cuda()
-        ev = torch.from_numpy(np.ascontiguousarray(events, np.uint64).view(np.int64)).cuda()
-        out = torch.empty(ev.numel(), dtype=torch.float32, device='cuda')
-        torch.cuda.synchronize()  # the uploads run on torch's stream, the kernel on the context's
+        dev = self.torch_device()
+        ph = torch.from_numpy(np.ascontiguousarray(phase, np.float32)).to(dev)
+        ev = torch.from_numpy(np.ascontiguousarray(events, np.uint64).view(np.int64)).to(dev)
+        out = torch.empty(ev.numel(), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize(dev)  # the uploads run on torch's stream, the kernel on the context's
         self.pulse_heights_device(ph, ph.shape[0], j0, ev, ev.numel(), out)
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(dev)
         return out.cpu().numpy()
 
     # ---- timing ------------------------------------------------------------------------------
@@ -214,6 +250,10 @@ class Channelizer:
             self._chk(self._L.mkid_get_timing(self._h, k, ctypes.byref(ms), ctypes.byref(n)))
             out[self._L.mkid_kernel_name(k).decode()] = (ms.value, n.value)
         return out
+
+    def stream_copy(self, d_dst, d_src, nbytes):
+        """Diagnostic HBM copy (mkid_stream_copy), asynchronous on the context stream."""
+        self._chk(self._L.mkid_stream_copy(self._h, _ptr(d_dst), _ptr(d_src), int(nbytes)))
 
     # ---- synthetic source (tests / bench only) -------------------------------------------------
     def synth_adc(self, d_out, nsamples, n0, d_base, d_tones, d_pulses, npulses, tau_rise,

@@ -214,14 +214,9 @@ bool channelize_supported(int N) {
 template <int N>
 static hipError_t launch_n(const ChanArgs& a0, hipStream_t s) {
     using G = Geo<N>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_channelize<N>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)G::lds_bytes);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_channelize<N>, (int)G::lds_bytes);
+    if (e != hipSuccess) return e;
     ChanArgs a = a0;
     if (a.K <= 0) return hipSuccess;
     // contiguous frame runs: long enough to amortise the (2T-1)-hop warm-up, enough runs to

@@ -372,13 +372,9 @@ int64_t front_hist_samples(int N) { return (int64_t)(2 * kPfbTaps - 1 + kLpfHist
 template <int N>
 static hipError_t launch_front_n(const FrontArgs& a0, hipStream_t s) {
     using G = FGeo<N>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_front<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)G::lds_bytes);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front<N>, (int)G::lds_bytes);
+    if (e != hipSuccess) return e;
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
     // frame runs: long enough to amortise the 24-frame warm-up, enough of them to fill the CUs

@@ -15,31 +15,36 @@ namespace mkid {
 
 constexpr int kHeightWaves = 4;  // packets (waves) per 256-thread workgroup
 
+// Grid-stride over packets: the count can be a device value (the trigger's written count,
+// a.d_n) so that a step launches with no host round trip; waves beyond it exit at once.
 __global__ __launch_bounds__(64 * kHeightWaves) void k_pulse_heights(HeightArgs a) {
-    const int64_t p = (int64_t)blockIdx.x * kHeightWaves + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (p >= a.n) return;  // wave-uniform: the whole wave leaves
-    const uint64_t w = a.events[p];
-    const int ch = (int)((w >> MKID_PKT_CH_SHIFT) & 0xFFF);
-    const int64_t ts = (int64_t)(w & MKID_PKT_TS_MASK);
-    // global phase index of the packet: the 28-bit stamp unwrapped against the rows' origin j0
-    const int64_t jg = a.j0 + ((ts - (a.j0 & (int64_t)MKID_PKT_TS_MASK)) & (int64_t)MKID_PKT_TS_MASK);
-    const int64_t r0 = jg - a.j0 - a.pre;  // first phase row of the window
-    const bool inside = ch < a.C && r0 >= 0 && r0 + a.ncoeff <= a.rows;
-    float acc = 0.f;
-    if (inside) {
-        const float* cf = a.coeff + (size_t)ch * a.ncoeff;
-        const float* ph = a.phase + r0 * a.C + ch;
-        for (int i = lane; i < a.ncoeff; i += 64) acc = fmaf(cf[i], ph[(int64_t)i * a.C], acc);
-    }
+    const int64_t n = a.d_n ? (*a.d_n < a.n ? *a.d_n : a.n) : a.n;
+    const int64_t nw = (int64_t)gridDim.x * kHeightWaves;
+    for (int64_t p = (int64_t)blockIdx.x * kHeightWaves + (threadIdx.x >> 6); p < n; p += nw) {
+        const uint64_t w = a.events[p];
+        const int ch = (int)((w >> MKID_PKT_CH_SHIFT) & 0xFFF);
+        const int64_t ts = (int64_t)(w & MKID_PKT_TS_MASK);
+        // global phase index of the packet: the 28-bit stamp unwrapped against the rows' origin j0
+        const int64_t jg = a.j0 + ((ts - (a.j0 & (int64_t)MKID_PKT_TS_MASK)) & (int64_t)MKID_PKT_TS_MASK);
+        const int64_t r0 = jg - a.j0 - a.pre;  // first phase row of the window
+        const bool inside = ch < a.C && r0 >= 0 && r0 + a.ncoeff <= a.rows;
+        float acc = 0.f;
+        if (inside) {
+            const float* cf = a.coeff + (size_t)ch * a.ncoeff;
+            const float* ph = a.phase + r0 * a.C + ch;
+            for (int i = lane; i < a.ncoeff; i += 64) acc = fmaf(cf[i], ph[(int64_t)i * a.C], acc);
+        }
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
-    if (lane == 0) a.heights[p] = inside ? acc : __builtin_nanf("");
+        for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+        if (lane == 0) a.heights[p] = inside ? acc : __builtin_nanf("");
+    }
 }
 
 hipError_t launch_pulse_heights(const HeightArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
-    const int64_t blocks = (a.n + kHeightWaves - 1) / kHeightWaves;
+    int64_t blocks = (a.n + kHeightWaves - 1) / kHeightWaves;
+    if (blocks > 256 * 32) blocks = 256 * 32;  // 8 waves per SIMD on every CU, then grid-stride
     hipLaunchKernelGGL(k_pulse_heights, dim3((unsigned)blocks), dim3(64 * kHeightWaves), 0, s, a);
     return hipGetLastError();
 }

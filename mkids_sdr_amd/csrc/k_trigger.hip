@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kSpecThreads, 3) void k_trig_spec(TrigSpecArgs a) {
     const int64_t jw = s == 0 ? 0 : seg0 - a.W;
     QWin win;
     load_qwin(win, a, c, jw);
-    const int64_t sc = (int64_t)c * a.nseg + s;
+    const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
     uint64_t* slot = a.slots + sc * a.capseg;
     int32_t n = 0;
     // all lanes of a wave share the segment (64 | C): a scalar row base and a 32-bit per-lane
@@ -169,38 +169,54 @@ __global__ __launch_bounds__(kSpecThreads, 3) void k_trig_spec(TrigSpecArgs a) {
     uint32_t roff = (uint32_t)(c >> 1) * 4u;  // byte offset of the lane's dword (C even)
     auto rload = [&](uint32_t off) { return *reinterpret_cast<const uint32_t*>(rbase + off); };
     QWin w0 = win;
-    Stepper<MODE> sp(s == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0}, k,
-                     mf_q(w0, tp, 0, rload(roff)));
-    // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0
-    run_groups(__builtin_amdgcn_readfirstlane((int32_t)(seg0 - jw) / kFirTaps), rbase, roff, (uint32_t)(2 * C), [&](int32_t, int u, uint32_t r) {
-        EvInfo ev;
-        (void)sp.step(mf_q(win, tp, u, r), ev);
-    });
-    if (s > 0) a.s_spec[(int64_t)s * C + c] = sp.state();
-    const int32_t len = (int32_t)(seg1 - seg0);
-    const int32_t full = len - len % kFirTaps;
-    run_groups(__builtin_amdgcn_readfirstlane(full / kFirTaps), rbase, roff, (uint32_t)(2 * C), [&](int32_t gr, int u, uint32_t r) {
-        const int32_t f = mf_q(win, tp, u, r);
-        EvInfo ev;
-        if (sp.step(f, ev)) {
-            if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gr * kFirTaps + u);
-            ++n;
-        }
-    });
-    const int32_t gi = full;
-    const int32_t left = len - gi;  // tail < 26 samples, predicated
+    const int32_t f0 = mf_q(w0, tp, 0, rload(roff));
+    const TrigState st0 = s == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
+    auto body = [&](auto& sp) {
+        // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0
+        run_groups(__builtin_amdgcn_readfirstlane((int32_t)(seg0 - jw) / kFirTaps), rbase, roff, (uint32_t)(2 * C),
+                   [&](int32_t, int u, uint32_t r) {
+                       EvInfo ev;
+                       (void)sp.step(mf_q(win, tp, u, r), ev);
+                   });
+        if (s > 0) a.s_spec[(int64_t)s * C + c] = sp.state();
+        const int32_t len = (int32_t)(seg1 - seg0);
+        const int32_t full = len - len % kFirTaps;
+        run_groups(__builtin_amdgcn_readfirstlane(full / kFirTaps), rbase, roff, (uint32_t)(2 * C),
+                   [&](int32_t gr, int u, uint32_t r) {
+                       const int32_t f = mf_q(win, tp, u, r);
+                       EvInfo ev;
+                       if (sp.step(f, ev)) {
+                           if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gr * kFirTaps + u);
+                           ++n;
+                       }
+                   });
+        const int32_t gi = full;
+        const int32_t left = len - gi;  // tail < 26 samples, predicated
 #pragma unroll
-    for (int u = 0; u < kFirTaps; ++u) {
-        if (u < left) {
-            const int32_t f = mf_q(win, tp, u, rload(roff + (uint32_t)(2 * u * C)));
-            EvInfo ev;
-            if (sp.step(f, ev)) {
-                if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);
-                ++n;
+        for (int u = 0; u < kFirTaps; ++u) {
+            if (u < left) {
+                const int32_t f = mf_q(win, tp, u, rload(roff + (uint32_t)(2 * u * C)));
+                EvInfo ev;
+                if (sp.step(f, ev)) {
+                    if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);
+                    ++n;
+                }
             }
         }
+        a.s_end[(int64_t)s * C + c] = sp.state();
+    };
+    if constexpr (MODE != MKID_BASE_SVF) {
+        if (in_holdoff(st0)) {  // first segment after a reset: the generic recurrence
+            Stepper<MODE, false> sp(st0, k, f0);
+            body(sp);
+        } else {
+            Stepper<MODE> sp(st0, k, f0);
+            body(sp);
+        }
+    } else {
+        Stepper<MODE> sp(st0, k, f0);
+        body(sp);
     }
-    a.s_end[(int64_t)s * C + c] = sp.state();
     a.counts[sc] = n;
 }
 
@@ -241,7 +257,7 @@ __device__ bool rerun_segment(const TrigSpecArgs& a, int c, int s, const int32_t
             merged = state_eq(tru, spc, a.mode);
         }
     }
-    const int64_t sc = (int64_t)c * a.nseg + s;
+    const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
     uint64_t* slot = a.slots + sc * a.capseg;
     const int32_t cnt = a.counts[sc] < a.capseg ? a.counts[sc] : a.capseg;
     int32_t total = nt;

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -17,7 +18,9 @@ using namespace mkid;
 
 namespace {
 
-std::string g_err;
+// error text of a failed mkid_create (no context yet); per thread, so that contexts created
+// concurrently from several host threads do not overwrite each other's message
+thread_local std::string g_err;
 
 // Default IQ low-pass: LUT/BlackmanFilter_250kHz.txt quantised as int(x*(2**11-1))
 // (ROACH_Pulses.py:69, 88; importFIRcoeffs default ROACH_Pulses.py:1101).
@@ -97,6 +100,7 @@ struct mkid_ctx {
     uint64_t* d_scratch = nullptr;   // [C][capseg]
     int32_t* d_reruns = nullptr;     // [C]
     int64_t nseg_max = 0, slot_cap = 0, scratch_cap = 0, trig_slots = 0;
+    int64_t nsub_max = 0;    // sub-chunks per call (ceil(max_chunk / G))
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
     int64_t last_J = 0;     // phase rows of the last call
     int64_t last_subJ = 0;  // rows of its last sub-chunk (held in d_raw)
@@ -255,7 +259,22 @@ static int quantize_pfb(const float* h, int T, int N, std::vector<int16_t>& hq) 
         while (S < 64 && std::ldexp(ms, S + 1) <= 65535.0 && std::ldexp(ma, S + 1) <= 32767.0) ++S;
     }
     hq.resize((size_t)T * N);
-    for (size_t i = 0; i < hq.size(); ++i) hq[i] = (int16_t)std::rint(std::ldexp((double)h[i], S));
+    // rounding can push a point's sum of |h_q| past 65535 (and a dot product of full-scale
+    // samples past INT32_MAX): step S down until the ROUNDED taps obey both bounds
+    for (;; --S) {
+        for (size_t i = 0; i < hq.size(); ++i) hq[i] = (int16_t)std::rint(std::ldexp((double)h[i], S));
+        bool ok = true;
+        for (int p = 0; p < N && ok; ++p) {
+            int64_t sp = 0;
+            for (int t = 0; t < T; ++t) {
+                const double r = std::rint(std::ldexp((double)h[t * N + p], S));
+                if (std::fabs(r) > 32767.0) ok = false;
+                sp += (int64_t)std::fabs(r);
+            }
+            if (sp > 65535) ok = false;
+        }
+        if (ok || S <= -64) break;
+    }
     return S;
 }
 
@@ -311,6 +330,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->G = G;
     c->Kmax = G / c->M;
     c->Jmax = G / N;
+    c->nsub_max = (cfg->max_chunk + G - 1) / G;
     // Packet capacities are hard bounds: an event needs >= dead_time + 3 phase samples (trigger,
     // peak, dead time, re-arm), so no per-channel/segment overflow can occur.
     const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // whole call, one segment
@@ -322,7 +342,8 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     // for J <= Jmax: L(J) <= Lmax and ceil(J / L(J)) <= max(slots * 64 / C, ceil(Jmax / kSegL))
     c->nseg_max = std::max<int64_t>(std::max<int64_t>(1, c->trig_slots * 64 / C), (c->Jmax + kSegL - 1) / kSegL);
     const int64_t capseg = seg_capacity(Lmax, cfg->dead_time);
-    c->slot_cap = std::max<int64_t>((int64_t)C * c->nseg_max * capseg, (int64_t)C * c->capc);
+    // one [C][sum of the sub-chunks' segments][capseg] table per call (single compaction)
+    c->slot_cap = (int64_t)C * c->nsub_max * std::max<int64_t>(c->nseg_max * capseg, c->capc);
     c->scratch_cap = std::max<int64_t>(capseg, c->capc);
     c->H = c->fused ? front_hist_samples(N) : (int64_t)c->T * N - c->M;
     const int64_t H = c->H;
@@ -365,8 +386,8 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_iqtap, (size_t)(cfg->max_chunk / N) * 2);
     AL(d_ysum, (size_t)2 * C);
     AL(d_slots, (size_t)c->slot_cap);
-    AL(d_chcounts, (size_t)C * c->nseg_max);
-    AL(d_scan, (size_t)C * c->nseg_max + 64);  // >= 3 int64 per compaction tile
+    AL(d_chcounts, (size_t)C * c->nsub_max * c->nseg_max);
+    AL(d_scan, (size_t)C * c->nsub_max * c->nseg_max + 64);  // >= 3 int64 per compaction tile
     AL(d_sspec, (size_t)C * c->nseg_max);
     AL(d_send, (size_t)C * c->nseg_max);
     AL(d_scratch, (size_t)C * c->scratch_cap);
@@ -553,7 +574,12 @@ int mkid_reset_stream(mkid_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->d_xhist, 0, (size_t)c->H * 4, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_zhist, 0, (size_t)kLpfHist * c->C * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_rhist, 0, (size_t)kRawHist * c->C * 2, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->d_tstate, 0, (size_t)c->C * sizeof(TrigState), c->stream));
+    {   // start-of-stream hold-off: DEAD for kHoldOff samples, no baseline (trig_common.h)
+        std::vector<TrigState> st0((size_t)c->C, TrigState{0, 0, 2 /*ST_DEAD*/, kHoldOff, 0, 0, 0, 0, 0, 0});
+        HIPCHK(c, hipMemcpyAsync(c->d_tstate, st0.data(), st0.size() * sizeof(TrigState), hipMemcpyHostToDevice,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 16, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->k0 = 0;
@@ -563,47 +589,85 @@ int mkid_reset_stream(mkid_ctx* c) {
     return MKID_OK;
 }
 
-// K7 + K8 on stream s for the J phase rows in d_raw: matched filter, baseline, trigger state
-// machine (speculative segments + fix-up), raw-phase history roll, packet compaction.
-static int run_trigger(mkid_ctx* c, int64_t J, uint64_t* d_events, int64_t cap, int64_t* d_counts,
-                       hipStream_t s) {
+// Trigger geometry of one sub-chunk of J phase rows: segment length L, warm-up W, nseg segments
+// and the per-segment packet capacity.
+struct SubPlan {
+    int64_t J;
+    int32_t L, W, nseg, capseg;
+};
+
+static SubPlan plan_sub(const mkid_ctx* c, int64_t J) {
+    const bool serial = c->mode == MKID_BASE_SVF || J <= kSegL;
+    const int64_t Ls = serial ? J : seg_length(J, c->C, c->trig_slots);
+    SubPlan p;
+    p.J = J;
+    p.L = (int32_t)Ls;
+    p.W = serial ? 0 : (int32_t)kSegW;
+    p.nseg = (int32_t)((J + Ls - 1) / Ls);
+    p.capseg = (int32_t)seg_capacity(Ls, c->cfg.dead_time);
+    return p;
+}
+
+// The sub-chunk plans of a call of n samples and the call's slot-table geometry: stride = total
+// segments per channel, capseg = the largest per-segment capacity (the table is uniform).
+static void plan_call(const mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, int32_t& stride, int32_t& capseg) {
+    subs.clear();
+    stride = 0;
+    capseg = 1;
+    for (int64_t off = 0; off < n; off += c->G) {
+        subs.push_back(plan_sub(c, std::min<int64_t>(c->G, n - off) / c->N));
+        stride += subs.back().nseg;
+        capseg = std::max(capseg, subs.back().capseg);
+    }
+}
+
+// K7 on stream s for the sub-chunk's phase rows in d_raw: matched filter, baseline, trigger state
+// machine (speculative segments + fix-up) into segments seg_off.. of the call's slot table, then
+// the raw-phase history roll. Compaction (K8) runs once per call (compact_call).
+static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32_t stride, int32_t seg_off,
+                       int32_t capseg, hipStream_t s) {
     const int C = c->C;
     KTime kt;
-    const bool serial = c->mode == MKID_BASE_SVF || J <= kSegL;
-    const int64_t Ls = serial ? J : seg_length(J, C, c->trig_slots);
-    const int32_t L = (int32_t)Ls;
-    const int32_t W = serial ? 0 : (int32_t)kSegW;
-    const int32_t nseg = (int32_t)((J + Ls - 1) / Ls);
-    const int32_t capseg = (int32_t)seg_capacity(Ls, c->cfg.dead_time);
-    TrigSpecArgs ta{c->d_raw,   c->d_rhist, c->d_fir,  c->d_thr,     c->d_tstate,  c->d_tstate,
+    TrigSpecArgs ta{raw,        c->d_rhist, c->d_fir,   c->d_thr,      c->d_tstate,  c->d_tstate,
                     c->d_sspec, c->d_send,  c->d_slots, c->d_chcounts, c->d_scratch, c->d_reruns,
-                    J,          c->j0,      C,          nseg,          L,            W,
+                    sp.J,       c->j0,      C,          sp.nseg,       sp.L,         sp.W,
                     capseg,     c->mode,    c->alpha,   c->kf,         c->kq,        c->base_thr,
-                    c->cfg.dead_time};
+                    c->cfg.dead_time, stride, seg_off};
     tstart(c, MKID_K_TRIGGER, &kt, s);
     HIPCHK(c, launch_trigger(ta, s));
     tstop(c, &kt, s);
-    HIPCHK(c, launch_hist_roll(c->d_rtmp, c->d_rhist, c->d_raw, kRawHist, J, (int64_t)C * 2, s));
+    HIPCHK(c, launch_hist_roll(c->d_rtmp, c->d_rhist, raw, kRawHist, sp.J, (int64_t)C * 2, s));
     HIPCHK(c, hipMemcpyAsync(c->d_rhist, c->d_rtmp, (size_t)kRawHist * C * 2, hipMemcpyDeviceToDevice, s));
+    return MKID_OK;
+}
 
+// K8: one compaction over the call's [C][stride] slot table -> channel-major, time-ascending.
+static int compact_call(mkid_ctx* c, int32_t stride, int32_t capseg, uint64_t* d_events, int64_t cap,
+                        int64_t* d_counts, hipStream_t s) {
+    KTime kt;
     tstart(c, MKID_K_COMPACT, &kt, s);
-    HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, (int64_t)C * nseg, capseg, d_events, cap, d_counts,
+    HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, (int64_t)c->C * stride, capseg, d_events, cap, d_counts,
                              c->d_scan, s));
     tstop(c, &kt, s);
     return MKID_OK;
 }
 
-// Fused front end: one k_front launch per chunk (ADC -> phase, raw), then K7/K8, all on the
-// context stream; chunks of max_chunk samples.
+// Fused front end: one k_front launch per sub-chunk (ADC -> phase, raw), then K7, all on the
+// context stream; one compaction per call.
 static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
                          int64_t cap, int64_t* d_counts) {
     const int C = c->C, N = c->N, M = c->M;
     hipStream_t s = c->stream;
+    std::vector<SubPlan> subs;
+    int32_t stride = 0, capseg = 0;
+    plan_call(c, n, subs, stride, capseg);
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
     HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, s));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
-    for (int64_t off = 0; off < n; off += c->G) {
+    int32_t seg_off = 0;
+    size_t si = 0;
+    for (int64_t off = 0; off < n; off += c->G, ++si) {
         const int64_t S = std::min<int64_t>(c->G, n - off);
         const int64_t K = S / M, J = S / N;
         KTime kt;
@@ -628,12 +692,17 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         tstart(c, MKID_K_FRONT, &kt, s);
         HIPCHK(c, launch_front(N, fa, s));
         tstop(c, &kt, s);
-        int r = run_trigger(c, J, d_events, cap, d_counts, s);
+        int r = run_trigger(c, c->d_raw, subs[si], stride, seg_off, capseg, s);
         if (r) return r;
+        seg_off += subs[si].nseg;
         c->k0 += K;
         c->j0 += J;
         c->last_J += J;
         c->last_subJ = J;
+    }
+    {
+        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, s);
+        if (r) return r;
     }
     HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, c->H, n, 4, s));
     HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)c->H * 4, hipMemcpyDeviceToDevice, s));
@@ -645,12 +714,17 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
                         int64_t cap, int64_t* d_counts) {
     if (!c || !d_iq || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
     if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
+    // the workspace (raw rows, IQ tap, slot table) is sized for max_chunk samples per call
+    if (n > c->cfg.max_chunk) FAIL(c, MKID_E_ARG, "nsamples exceeds cfg.max_chunk");
     if (((uintptr_t)d_iq & 15) != 0) FAIL(c, MKID_E_ARG, "d_iq must be 16-byte aligned");
     HIPCHK(c, hipSetDevice(c->device));
     if (c->fused) return process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts);
     const int C = c->C, N = c->N, M = c->M;
     const int64_t H = c->H;
     hipStream_t A = c->stream, B = c->sB;
+    std::vector<SubPlan> subs;
+    int32_t stride = 0, capseg = 0;
+    plan_call(c, n, subs, stride, capseg);
     // B joins A's order (inputs written by earlier work on A, previous calls) ...
     HIPCHK(c, hipEventRecord(c->ev_start, A));
     HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
@@ -658,8 +732,10 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, B));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
+    int32_t seg_off = 0;
+    size_t si = 0;
     const float2* zprev = c->d_zhist;  // the 24 frames before the current sub-chunk
-    for (int64_t off = 0; off < n; off += c->G) {
+    for (int64_t off = 0; off < n; off += c->G, ++si) {
         const int64_t S = std::min<int64_t>(c->G, n - off);
         const int64_t K = S / M, J = S / N;
         const int b = c->zi;
@@ -673,7 +749,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
         tstop(c, &kt, A);
         HIPCHK(c, hipEventRecord(c->ev_zready[b], A));
 
-        // ---- stream B: low-pass + phase, trigger, compaction of this sub-chunk ----
+        // ---- stream B: low-pass + phase and trigger of this sub-chunk ----
         HIPCHK(c, hipStreamWaitEvent(B, c->ev_zready[b], 0));
         LpfArgs la{z, zprev, c->d_ic, c->d_qc, d_phase ? d_phase + (off / N) * C : nullptr,
                    c->d_raw, c->d_ysum, J, C, c->lpf,
@@ -696,13 +772,18 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
         c->zi ^= 1;
 
         {
-            int r = run_trigger(c, J, d_events, cap, d_counts, B);
+            int r = run_trigger(c, c->d_raw, subs[si], stride, seg_off, capseg, B);
             if (r) return r;
         }
+        seg_off += subs[si].nseg;
         c->k0 += K;
         c->j0 += J;
         c->last_J += J;
         c->last_subJ = J;
+    }
+    {
+        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, B);
+        if (r) return r;
     }
     // ADC history for the next call (all readers of d_xhist are channeliser launches on A)
     HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, H, n, 4, A));
@@ -712,6 +793,29 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     HIPCHK(c, hipStreamWaitEvent(A, c->ev_done, 0));
     c->iq_rows = c->iq_ch >= 0 ? n / N : 0;
     return MKID_OK;
+}
+
+int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t* d_events, int64_t cap,
+                       int64_t* d_counts) {
+    if (!c || !d_raw || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
+    if (rows <= 0 || rows > c->cfg.max_chunk / c->N) FAIL(c, MKID_E_ARG, "rows must be in 1 .. max_chunk/N");
+    if (((uintptr_t)d_raw & 3) != 0) FAIL(c, MKID_E_ARG, "d_raw must be 4-byte aligned");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    std::vector<SubPlan> subs;
+    int32_t stride = 0, capseg = 0;
+    plan_call(c, rows * c->N, subs, stride, capseg);
+    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
+    int32_t seg_off = 0;
+    int64_t r0 = 0;
+    for (const SubPlan& sp : subs) {
+        int r = run_trigger(c, d_raw + r0 * c->C, sp, stride, seg_off, capseg, s);
+        if (r) return r;
+        seg_off += sp.nseg;
+        r0 += sp.J;
+        c->j0 += sp.J;
+    }
+    return compact_call(c, stride, capseg, d_events, cap, d_counts, s);
 }
 
 int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, uint64_t* events_out, int64_t cap,
@@ -930,14 +1034,40 @@ int mkid_set_pulse_filter(mkid_ctx* c, const float* coeff, int32_t nch, int32_t 
     return upload(c, c->d_hcoeff, coeff, (size_t)nch * ncoeff * 4);
 }
 
-int mkid_pulse_heights(mkid_ctx* c, const float* d_phase, int64_t rows, int64_t j0, const uint64_t* d_events,
-                       int64_t n, float* d_heights) {
+static int pulse_heights(mkid_ctx* c, const float* d_phase, int64_t rows, int64_t j0, const uint64_t* d_events,
+                         const int64_t* d_n, int64_t n, float* d_heights) {
     if (!c || (n > 0 && (!d_phase || !d_events || !d_heights))) return MKID_E_ARG;
     if (rows < 0 || j0 < 0 || n < 0) FAIL(c, MKID_E_ARG, "pulse heights: negative rows/j0/n");
     if (!c->d_hcoeff) FAIL(c, MKID_E_STATE, "pulse heights: no filter set (mkid_set_pulse_filter)");
     HIPCHK(c, hipSetDevice(c->device));
-    HeightArgs a{d_phase, d_events, c->d_hcoeff, d_heights, rows, j0, n, c->C, c->h_ncoeff, c->h_pre};
+    HeightArgs a{d_phase, d_events, c->d_hcoeff, d_heights, rows, j0, n, c->C, c->h_ncoeff, c->h_pre, d_n};
+    KTime kt;
+    tstart(c, MKID_K_HEIGHTS, &kt, c->stream);
     HIPCHK(c, launch_pulse_heights(a, c->stream));
+    tstop(c, &kt, c->stream);
+    return MKID_OK;
+}
+
+int mkid_pulse_heights(mkid_ctx* c, const float* d_phase, int64_t rows, int64_t j0, const uint64_t* d_events,
+                       int64_t n, float* d_heights) {
+    return pulse_heights(c, d_phase, rows, j0, d_events, nullptr, n, d_heights);
+}
+
+int mkid_pulse_heights_counted(mkid_ctx* c, const float* d_phase, int64_t rows, int64_t j0,
+                               const uint64_t* d_events, const int64_t* d_count, int64_t cap, float* d_heights) {
+    if (!d_count) return MKID_E_ARG;
+    return pulse_heights(c, d_phase, rows, j0, d_events, d_count, cap, d_heights);
+}
+
+int mkid_stream_copy(mkid_ctx* c, void* d_dst, const void* d_src, int64_t bytes) {
+    if (!c || !d_dst || !d_src || bytes < 0) return MKID_E_ARG;
+    if (bytes % 16 != 0 || ((uintptr_t)d_dst & 15) != 0 || ((uintptr_t)d_src & 15) != 0)
+        FAIL(c, MKID_E_ARG, "stream copy: 16-byte aligned pointers and sizes only");
+    HIPCHK(c, hipSetDevice(c->device));
+    KTime kt;
+    tstart(c, MKID_K_COPY, &kt, c->stream);
+    HIPCHK(c, launch_stream_copy(d_dst, d_src, bytes, c->stream));
+    tstop(c, &kt, c->stream);
     return MKID_OK;
 }
 
@@ -960,7 +1090,8 @@ int mkid_get_timing(mkid_ctx* c, int32_t k, double* total_ms, int64_t* launches)
 }
 
 const char* mkid_kernel_name(int32_t k) {
-    static const char* names[MKID_K_COUNT] = {"k_channelize", "k_lpf_phase", "k_trigger", "k_compact", "k_front"};
+    static const char* names[MKID_K_COUNT] = {"k_channelize", "k_lpf_phase", "k_trigger", "k_compact",
+                                              "k_front",      "k_stream_copy", "k_pulse_heights"};
     return (k >= 0 && k < MKID_K_COUNT) ? names[k] : "?";
 }
 

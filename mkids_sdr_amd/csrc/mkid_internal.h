@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -14,6 +15,10 @@ constexpr int kPfbTaps = 4;    // T: PFB taps per branch (build decision, DESIGN
 constexpr int kFirTaps = 26;   // ROACH_Pulses.py:61
 constexpr int kLpfHist = kFirTaps - 2;  // z frames carried for the decimating IQ low-pass
 constexpr int kRawHist = kFirTaps - 1;  // raw phase samples carried for the matched filter
+// Start-of-stream trigger hold-off (phase samples): after a reset the trigger is DEAD with no
+// baseline while the PFB / low-pass / matched-filter histories fill (build decision, DESIGN.md §2;
+// oracle/trigger.c HOLDOFF)
+constexpr int kHoldOff = 64;
 
 // Per-channel trigger state. Byte layout identical to oracle/trigger.c trig_state.
 struct TrigState {
@@ -103,14 +108,17 @@ struct TrigSpecArgs {
     TrigState* st_out;      // [C] carried state after this call (may alias st_in)
     TrigState* s_spec;      // [nseg][C] speculative state at each segment start
     TrigState* s_end;       // [nseg][C] state at each segment end
-    uint64_t* slots;        // [C][nseg][capseg] packets
-    int32_t* counts;        // [C][nseg]
+    uint64_t* slots;        // [C][seg_stride][capseg] packets (entry c*seg_stride + seg_off + s)
+    int32_t* counts;        // [C][seg_stride]
     uint64_t* scratch;      // [C][capseg] fix-up scratch
     int32_t* reruns;        // [C] segments re-run by the fix-up (diagnostic, nullable)
     int64_t J;
     int64_t j0;             // global index of the chunk's first phase sample
     int32_t C, nseg, L, W, capseg;
     int32_t mode, alpha, kf, kq, base_thr, dead;
+    // the segments of one call's sub-chunks share one [C][seg_stride] slot table, so that a single
+    // compaction at the end of the call orders packets channel-major over the whole call
+    int32_t seg_stride, seg_off;
 };
 
 struct HeightArgs {
@@ -118,8 +126,9 @@ struct HeightArgs {
     const uint64_t* events;  // [n] wide packets
     const float* coeff;      // [C][ncoeff] per-channel optimal filter
     float* heights;          // [n] out (NaN: window outside the rows or unknown channel)
-    int64_t rows, j0, n;
+    int64_t rows, j0, n;    // n: packets (or the bound on *d_n)
     int32_t C, ncoeff, pre;
+    const int64_t* d_n;     // nullable: device packet count (min(*d_n, n) packets are processed)
 };
 
 // launchers (return hipError_t of the launch)
@@ -135,6 +144,7 @@ hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t 
                           int64_t* scan_ws, hipStream_t s);
 hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
                             int64_t fresh_rows, int64_t row_bytes, hipStream_t s);
+hipError_t launch_stream_copy(void* dst, const void* src, int64_t bytes, hipStream_t s);
 hipError_t launch_synth(int16_t* out, int64_t n, int64_t n0, const int16_t* base,
                         const mkid_synth_tone* tones, const mkid_pulse* pulses, int64_t npulses,
                         float tr, float tf, int32_t window, float sigma, uint32_t seed,
@@ -149,6 +159,20 @@ hipError_t launch_make_template(float* I, float* Q, int64_t P, double* rows, dou
                                 double* noise, double* stats, float* refmed, hipStream_t s);
 hipError_t launch_optimal_filter(const double* tpl, const double* noise, int pre, int ncoeff, double* coeff,
                                  double* work, hipStream_t s);
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device), thread-safe: the
+// attribute is per device, and several contexts (devices, host threads) may launch concurrently.
+// `mask` is one static per kernel instantiation; the call is idempotent, so a race only repeats it.
+inline hipError_t ensure_lds_attr(std::atomic<uint64_t>& mask, const void* fn, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (mask.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) mask.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
 
 bool channelize_supported(int N);
 bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length

@@ -44,7 +44,9 @@ __device__ __attribute__((noinline)) uint64_t make_packet(int32_t c, EvInfo ev, 
 // Advance state s by one filtered sample f. Returns true when a packet is due; ev then holds
 // its inputs (the packet is stamped jg - 1: the peak is the previous sample).
 __device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigCfg& k, EvInfo& ev) {
-    if (!s.binit) {
+    // the baseline starts at the first sample after the start-of-stream hold-off (a reset leaves
+    // the state DEAD for kHoldOff samples with no baseline, oracle/trigger.c HOLDOFF)
+    if (!s.binit && s.st != ST_DEAD) {
         s.B = (k.mode == MKID_BASE_NONE) ? 0 : f;
         s.low = (int64_t)f << 16;
         s.band = 0;
@@ -53,9 +55,9 @@ __device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigC
     const int32_t base_prev = (k.mode == MKID_BASE_SVF) ? (int32_t)(s.low >> 16) : s.B;
     const int32_t e = f - base_prev;
     const bool gate = (k.base_thr <= 0) || (e < k.base_thr && e > -k.base_thr);
-    if (k.mode == MKID_BASE_EMA) {
+    if (k.mode == MKID_BASE_EMA && s.binit) {
         s.B += gate ? ((k.alpha * e) >> 9) : 0;
-    } else if (k.mode == MKID_BASE_SVF && gate) {
+    } else if (k.mode == MKID_BASE_SVF && gate && s.binit) {
         const int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)k.kq * s.band) >> 16);
         s.band += ((int64_t)k.kf * high) >> 16;
         s.low += ((int64_t)k.kf * s.band) >> 16;
@@ -75,6 +77,10 @@ __device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigC
     s.f1 = f;
     return emit;
 }
+
+// A state in the start-of-stream hold-off (DEAD, baseline not yet set) must run trig_update:
+// the fast form below assumes the baseline is settled.
+__device__ __forceinline__ bool in_holdoff(const TrigState& s) { return !s.binit && s.st == ST_DEAD; }
 
 // Hot-loop form of trig_update for the EMA and no-baseline modes (k_trig_spec), same outputs:
 //  * the state machine is one code x: ARMED -1, PULSE -2, REARM 0, DEAD = dead-time samples

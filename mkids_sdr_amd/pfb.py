@@ -24,4 +24,9 @@ def effective_taps(h, T=4):
         S = -64
         while S < 64 and np.ldexp(ms, S + 1) <= 65535.0 and np.ldexp(ma, S + 1) <= 32767.0:
             S += 1
-    return np.ldexp(np.rint(np.ldexp(h, S)), -S).reshape(-1), int(S)
+    while True:   # step S down until the rounded taps obey both bounds (mkid_set_pfb)
+        hq = np.rint(np.ldexp(h, S))
+        if (np.abs(hq).sum(axis=0).max() <= 65535 and np.abs(hq).max() <= 32767) or S <= -64:
+            break
+        S -= 1
+    return np.ldexp(hq, -S).reshape(-1), int(S)

@@ -46,7 +46,14 @@ def quantize_pfb(h, T, N):
         S = -64
         while S < 64 and np.ldexp(ms, S + 1) <= 65535.0 and np.ldexp(ma, S + 1) <= 32767.0:
             S += 1
-    hq = np.rint(np.ldexp(h, S))
+    # the device re-checks the ROUNDED taps and steps S down while a point's sum of |h_q|
+    # exceeds 65535 or a |h_q| exceeds 32767 (int16 dot products of full-scale samples stay
+    # inside int32, mkid_api.hip quantize_pfb)
+    while True:
+        hq = np.rint(np.ldexp(h, S))
+        if (np.abs(hq).sum(axis=0).max() <= 65535 and np.abs(hq).max() <= 32767) or S <= -64:
+            break
+        S -= 1
     return np.ldexp(hq, -S).reshape(-1), int(S)
 
 

@@ -16,6 +16,11 @@
 
 #define NT 26
 enum { ST_ARMED = 0, ST_PULSE = 1, ST_DEAD = 2, ST_REARM = 3 };
+/* Start-of-stream hold-off (build decision): after a reset the trigger state is
+ * DEAD for HOLDOFF samples with no baseline, so the filters' start-up transient (zero PFB / low-pass
+ * / matched-filter history) neither fires the trigger nor seeds the baseline; the baseline is
+ * initialised from the first sample after it. */
+#define HOLDOFF 64
 
 typedef struct {
     int32_t B, binit, st, cnt, f1, f2, pad0, pad1;
@@ -40,6 +45,15 @@ uint64_t pack_wide(int32_t ch, int64_t peak, int32_t base, int64_t j) {
     return ((uint64_t)(ch & 0xFFF) << 52) | (pk << 40) | (bs << 28) | ((uint64_t)j & ((1ull << 28) - 1));
 }
 
+/* State of a freshly reset channel: hold-off, no baseline yet. */
+void oracle_trig_reset_state(trig_state* st, int32_t C) {
+    memset(st, 0, sizeof(trig_state) * (size_t)C);
+    for (int32_t c = 0; c < C; ++c) {
+        st[c].st = ST_DEAD;
+        st[c].cnt = HOLDOFF;
+    }
+}
+
 /* raw: [J][C] int16 Fix16_13 time-major; hist: [25][C] previous raw (hist[24] = newest);
  * taps: [C][26] int12; st: [C]. Events are written channel-major, time-ascending; returns the
  * total number produced (may exceed cap; only cap are written). counts[c] (nullable) = per-ch. */
@@ -59,7 +73,7 @@ int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* 
                 acc += (int32_t)taps[c * NT + i] * r;
             }
             int32_t f = clamp16(acc >> 11);
-            if (!s.binit) {
+            if (!s.binit && s.st != ST_DEAD) { /* first sample after the hold-off */
                 s.B = (mode == 0) ? 0 : f;
                 s.low = (int64_t)f << 16;
                 s.band = 0;
@@ -68,9 +82,9 @@ int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* 
             int32_t base_prev = (mode == 2) ? (int32_t)(s.low >> 16) : s.B;
             int32_t e = f - base_prev;
             int gate = (base_thr <= 0) || (e < base_thr && e > -base_thr);
-            if (mode == 1 && gate) {
+            if (s.binit && mode == 1 && gate) {
                 s.B += (alpha * e) >> 9;
-            } else if (mode == 2 && gate) {
+            } else if (s.binit && mode == 2 && gate) {
                 int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)kq * s.band) >> 16);
                 s.band += ((int64_t)kf * high) >> 16;
                 s.low += ((int64_t)kf * s.band) >> 16;

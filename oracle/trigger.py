@@ -32,6 +32,8 @@ def lib():
                                      ctypes.c_int32, ctypes.c_int32, P, P, ctypes.c_int64, P,
                                      ctypes.c_int64, P]
         L.oracle_trig_state_size.restype = ctypes.c_int32
+        L.oracle_trig_reset_state.restype = None
+        L.oracle_trig_reset_state.argtypes = [P, ctypes.c_int32]
         assert L.oracle_trig_state_size() == STATE_DTYPE.itemsize
         _lib = L
     return _lib
@@ -55,6 +57,7 @@ class Trigger:
     def reset(self):
         self.hist = np.zeros((25, self.C), np.int16)
         self.state = np.zeros(self.C, STATE_DTYPE)
+        lib().oracle_trig_reset_state(_p(self.state), self.C)   # start-of-stream hold-off
         self.j0 = 0
 
     def run(self, raw, cap=None):

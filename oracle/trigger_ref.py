@@ -7,6 +7,7 @@ import numpy as np
 
 NT = 26
 ARMED, PULSE, DEAD, REARM = 0, 1, 2, 3
+HOLDOFF = 64      # start-of-stream hold-off (trigger.c HOLDOFF)
 
 
 def trunc_div(n, d):
@@ -34,7 +35,7 @@ def unpack_wide(w):
 
 
 def new_state(C):
-    return [dict(B=0, binit=0, st=ARMED, cnt=0, f1=0, f2=0, low=0, band=0) for _ in range(C)]
+    return [dict(B=0, binit=0, st=DEAD, cnt=HOLDOFF, f1=0, f2=0, low=0, band=0) for _ in range(C)]
 
 
 def trigger(raw, taps, thr, mode, alpha, kf, kq, base_thr, dead, hist=None, state=None, j0=0):
@@ -54,7 +55,7 @@ def trigger(raw, taps, thr, mode, alpha, kf, kq, base_thr, dead, hist=None, stat
             for i in range(NT):
                 acc += a[i] * col[25 + j - i]
             f = min(max(acc >> 11, -32768), 32767)
-            if not s['binit']:
+            if not s['binit'] and s['st'] != DEAD:
                 s['B'] = 0 if mode == 0 else f
                 s['low'] = f << 16
                 s['band'] = 0
@@ -62,9 +63,9 @@ def trigger(raw, taps, thr, mode, alpha, kf, kq, base_thr, dead, hist=None, stat
             base_prev = (s['low'] >> 16) if mode == 2 else s['B']
             e = f - base_prev
             gate = base_thr <= 0 or (-base_thr < e < base_thr)
-            if mode == 1 and gate:
+            if s['binit'] and mode == 1 and gate:
                 s['B'] += (alpha * e) >> 9
-            elif mode == 2 and gate:
+            elif s['binit'] and mode == 2 and gate:
                 high = (f << 16) - s['low'] - ((kq * s['band']) >> 16)
                 s['band'] += (kf * high) >> 16
                 s['low'] += (kf * s['band']) >> 16

@@ -22,8 +22,10 @@ class Case:
 
 def make_case(C, n_samples, fs=FS, n_tones=None, seed=0, noise=30.0, pulses_per_ch=0.0,
               amp_deg=(20.0, 100.0), tau_rise=0.1, tau_fall=65.0, window_phase=390,
-              pulse_margin=64):
-    """Return a Case with .iq int16 [S][2] and every configuration array both sides need."""
+              pulse_margin=64, dds_phase=None):
+    """Return a Case with .iq int16 [S][2] and every configuration array both sides need.
+    dds_phase [C] (rad): per-channel DDS LUT phase, e.g. rotateLoopsReady's arctan2 of the
+    average IQ (ROACH_Setup.py:645-667); the tones and noise do not depend on it."""
     N = 2 * C
     res = fs / LUT_LEN
     upb = LUT_LEN // N                       # fs/2^16 units per coarse bin
@@ -39,7 +41,8 @@ def make_case(C, n_samples, fs=FS, n_tones=None, seed=0, noise=30.0, pulses_per_
     lut_i = np.zeros((C, LUT_LEN // C), np.int64)
     lut_q = np.zeros((C, LUT_LEN // C), np.int64)
     for ch in range(C):
-        I, Q, _, _ = setup_ref.freq_comb_lut('no', [resid[ch]], fs / N * 2, res, [1.], [0.], 'no')
+        ph0 = 0. if dds_phase is None else float(dds_phase[ch])
+        I, Q, _, _ = setup_ref.freq_comb_lut('no', [resid[ch]], fs / N * 2, res, [1.], [ph0], 'no')
         lut_i[ch], lut_q[ch] = I, Q
 
     # DAC side: tone at -f_dds (mod fs), freqCombLUT('yes') with the reference's random phases
@@ -115,3 +118,43 @@ def thresholds_from_quiet(case, raw_quiet, nsigma=2.5):
 
 def wrap(d):
     return (d + np.pi) % (2 * np.pi) - np.pi
+
+
+def match_pulses(events, pulses, N, early=2, late=60, isolation=400):
+    """Score wide packets against injected truth (start ADC sample, channel, amplitude).
+    A packet of channel c stamped ts matches a pulse of c starting at phase row p when
+    p - early <= ts <= p + late. Returns dict: isolated (pulses with no other pulse of their
+    channel within `isolation` rows), exactly_one (isolated pulses with exactly one packet),
+    missed, multi, extra (packets matching no pulse)."""
+    ev = np.asarray(events, np.uint64)
+    ch = ((ev >> np.uint64(52)) & np.uint64(0xFFF)).astype(np.int64)
+    ts = (ev & np.uint64((1 << 28) - 1)).astype(np.int64)
+    by_ch = {}
+    for s0, c, _ in pulses:
+        by_ch.setdefault(int(c), []).append(int(s0) // N)
+    for c in by_ch:
+        by_ch[c] = np.sort(np.array(by_ch[c]))
+    hits = {}
+    extra = 0
+    for c, t in zip(ch, ts):
+        p = by_ch.get(int(c))
+        if p is None:
+            extra += 1
+            continue
+        k = np.searchsorted(p, t + early, side='right') - 1
+        if k >= 0 and p[k] - early <= t <= p[k] + late:
+            hits[(int(c), int(p[k]))] = hits.get((int(c), int(p[k])), 0) + 1
+        else:
+            extra += 1
+    iso = exactly = missed = multi = 0
+    for c, p in by_ch.items():
+        for i, r in enumerate(p):
+            if (i > 0 and r - p[i - 1] < isolation) or (i + 1 < len(p) and p[i + 1] - r < isolation):
+                continue
+            iso += 1
+            n = hits.get((c, int(r)), 0)
+            exactly += n == 1
+            missed += n == 0
+            multi += n > 1
+    return dict(isolated=iso, exactly_one=exactly, missed=missed, multi=multi, extra=extra,
+                packets=int(len(ev)), pulses=len(pulses))

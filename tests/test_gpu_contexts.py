@@ -1,0 +1,89 @@
+"""Context hygiene of the C ABI: several contexts in one process (and from several host threads)
+on the same GPU give the results one context gives alone; the device entry point rejects calls
+larger than its workspace; packets of a call are channel-major over the whole call."""
+import threading
+
+import numpy as np
+import pytest
+
+import signals
+from test_gpu_parity import configure, quiet_thresholds, sort_events
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(case, thr, out, key, max_chunk, splits):
+    from mkids_sdr_amd.channelizer import Channelizer
+    ch = Channelizer(case.C, max_chunk=max_chunk)
+    try:
+        configure(ch, case, thr)
+        ph, ev = [], []
+        for a, b in zip(splits[:-1], splits[1:]):
+            p, e = ch.process(case.iq[a:b])
+            ph.append(p)
+            ev.append(e)
+        out[key] = (np.concatenate(ph), np.concatenate(ev))
+    finally:
+        ch.close()
+
+
+def test_two_contexts_two_threads_same_gpu(gpu):
+    C, S = 256, 1 << 20
+    cases = [signals.make_case(C, S, seed=s, pulses_per_ch=3.0, noise=100.0) for s in (31, 32)]
+    thrs = [quiet_thresholds(C, S // 4, s) for s in (31, 32)]
+    splits = [0, S // 2, S]
+    alone = {}
+    for i in range(2):
+        _run(cases[i], thrs[i], alone, i, S, splits)
+    both = {}
+    ts = [threading.Thread(target=_run, args=(cases[i], thrs[i], both, i, S, splits)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for i in range(2):
+        assert np.array_equal(alone[i][0], both[i][0])
+        assert np.array_equal(alone[i][1], both[i][1])
+        assert len(alone[i][1]) > 0
+    # the two feedlines are different streams
+    assert not np.array_equal(alone[0][0], alone[1][0])
+
+
+def test_device_call_larger_than_workspace_is_rejected(gpu):
+    import torch
+    from mkids_sdr_amd import _lib
+    from mkids_sdr_amd.channelizer import Channelizer
+    C = 64
+    ch = Channelizer(C, max_chunk=1 << 14)
+    try:
+        ch.set_iq_tap(3)
+        n = 1 << 15
+        x = torch.zeros(2 * n, dtype=torch.int16, device='cuda')
+        ev = torch.empty(1024, dtype=torch.int64, device='cuda')
+        cnt = torch.zeros(2, dtype=torch.int64, device='cuda')
+        with pytest.raises(_lib.MkidError):
+            ch.process_device(x, n, None, ev, 1024, cnt)
+        ch.process_device(x, n // 2, None, ev, 1024, cnt)   # at the limit: fine
+        torch.cuda.synchronize()
+        assert ch.iq_tap().shape == (n // 2 // (2 * C), 2)
+    finally:
+        ch.close()
+
+
+@pytest.mark.parametrize('front', ['auto', 'split'])
+def test_packets_channel_major_over_whole_call(gpu, front):
+    """The split front end cuts a call into sub-chunks; packets still come out channel-major and
+    time-ascending over the whole call (one compaction per call)."""
+    from mkids_sdr_amd.channelizer import Channelizer
+    C = 256
+    S = 600 * 2 * C          # >= 512 N: four pipeline sub-chunks on the split path
+    case = signals.make_case(C, S, seed=41, pulses_per_ch=4.0, noise=100.0)
+    thr = quiet_thresholds(C, S // 4, 41)
+    ch = Channelizer(C, max_chunk=S, front=front)
+    try:
+        configure(ch, case, thr)
+        _, ev = ch.process(case.iq)
+    finally:
+        ch.close()
+    assert len(ev) > 100
+    assert np.array_equal(ev, sort_events(ev))

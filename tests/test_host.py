@@ -215,3 +215,47 @@ def test_pfb_tap_quantisation_matches_oracle(N):
         mine, Sm = pfb.effective_taps(h)
         assert S.value == Sr == Sm
         assert np.array_equal(out.astype(np.float64), ref) and np.array_equal(mine, ref)
+
+
+def test_pfb_rounding_cannot_overflow_the_int16_dot_products():
+    """A prototype whose unrounded per-point sum sits just under 65535 * 2^-S but whose ROUNDED
+    taps exceed it: the rule steps S down (full-scale -32768 samples aligned with the
+    tap signs would otherwise wrap the int32 v_dot2 chain)."""
+    import ctypes
+    from mkids_sdr_amd import _lib, pfb
+    from oracle.chain import quantize_pfb
+    N = 16
+    h = np.full(4 * N, 1e-3, np.float32)
+    h[[0 * N + 3, 1 * N + 3, 2 * N + 3, 3 * N + 3]] = np.float32(16383.6)   # point 3: 4 x 16383.6
+    out = np.empty(4 * N, np.float32)
+    S = ctypes.c_int32()
+    assert _lib.load().mkid_pfb_effective_taps(h.ctypes.data_as(ctypes.c_void_p), 4, N,
+                                                out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(S)) == 0
+    ref, Sr = quantize_pfb(h, 4, N)
+    mine, Sm = pfb.effective_taps(h)
+    assert S.value == Sr == Sm == -1
+    hq = np.rint(np.ldexp(out.astype(np.float64), S.value)).reshape(4, N)
+    assert np.abs(hq).sum(axis=0).max() <= 65535 and np.abs(hq).max() <= 32767
+    assert 32768 * int(np.abs(hq).sum(axis=0).max()) <= 2 ** 31 - 1
+    assert np.array_equal(out.astype(np.float64), ref) and np.array_equal(mine, ref)
+
+
+def test_cpu_baseline_tool_runs(tmp_path):
+    """tools/cpu_baseline.py (bench.py's CPU leg) on a tiny input: one-core, all-core and C1."""
+    import json
+    import subprocess
+    import sys
+    import signals
+    c = signals.make_case(64, 1 << 16, seed=2, noise=30.0, pulses_per_ch=1.0)
+    np.save(tmp_path / 'in.npy', c.iq)
+    np.savez(tmp_path / 'cfg.npz', C=64, pfb=c.pfb, bins=c.bins, lut_i=c.lut_i, lut_q=c.lut_q,
+             lpf=c.lpf12, fir=c.fir12, thr=np.full(64, -300))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, 'tools', 'cpu_baseline.py'), '--input',
+                        str(tmp_path / 'in.npy'), '--cfg', str(tmp_path / 'cfg.npz'), '--one-core-samples',
+                        str(1 << 15), '--all-core-samples', str(1 << 16), '--workers', '2'],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out['one_core']['value'] > 0 and out['all_cores']['cores'] == 2 and out['c1']['value'] > 0
+    assert out['os_cpu_count'] >= 1 and out['cpu_model']

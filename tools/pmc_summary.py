@@ -53,6 +53,7 @@ def main():
     ap.add_argument('dir')
     ap.add_argument('--json')
     ap.add_argument('--samples-log2', type=int, default=28, help='ADC samples per launch in the PMC run')
+    ap.add_argument('--config', type=int, default=3, help='bench config the run measured (json key)')
     a = ap.parse_args()
     s = read(a.dir)
     res = {}
@@ -75,7 +76,10 @@ def main():
                    'hbm_bytes_per_sample': v.get('hbm_bytes_per_sample'),
                    'pmc_samples': 1 << a.samples_log2, 'source': a.dir}
                for k, v in res.items() if 'hbm_bytes_per_launch' in v}
-        json.dump(out, open(a.json, 'w'), indent=1)
+        rec = json.load(open(a.json)) if os.path.exists(a.json) else {}
+        rec = {k: v for k, v in rec.items() if k.startswith('config')}   # config-keyed layout
+        rec['config%d' % a.config] = out
+        json.dump(rec, open(a.json, 'w'), indent=1)
 
 
 if __name__ == '__main__':

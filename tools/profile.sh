@@ -1,18 +1,19 @@
 #!/bin/bash
 # rocprofv3 passes over bench.py on the GPU box (run through gpurun from the repo root):
-#   bash tools/profile.sh TAG
+#   bash tools/profile.sh TAG [extra bench.py args, e.g. --config 5]
 # 1. kernel trace + stats of the default bench workload (per-kernel average durations);
 # 2. PMC passes, each its own run (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950;
 #    counters are never combined with runtime/sys traces), on one default (2^30-sample) step.
 # Output: gpurun_out/prof_TAG/{kt,fetch,write,sq1,sq2}/...
 set -euo pipefail
 TAG=${1:-run}
+shift || true
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-B="python3 $ROOT/bench.py --no-cpu-baseline"
+B="python3 $ROOT/bench.py --no-cpu-baseline $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
     -- $B --steps 3 --warmup 1 > "$OUT/kt.log" 2>&1
 SMALL="--steps 1 --warmup 1"

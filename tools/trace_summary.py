@@ -7,13 +7,20 @@ bench.py launches its calibration passes on smaller inputs before the timed step
 grid size separates those from the timed launches, whose average must agree with the
 `avg_launch_ms` bench.py measures with HIP events.
 """
+import argparse
 import csv
-import sys
+import json
+import os
 from collections import defaultdict
 
 
 def main():
-    rows = list(csv.DictReader(open(sys.argv[1])))
+    ap = argparse.ArgumentParser()
+    ap.add_argument('csv')
+    ap.add_argument('--json', help='update this file: {"config<N>": {kernel: avg ms of its largest-grid launches}}')
+    ap.add_argument('--config', type=int, default=3)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.csv)))
     g = defaultdict(list)
     for r in rows:
         grid = int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) * int(r['Grid_Size_Z'])
@@ -22,6 +29,19 @@ def main():
     print('%-48s %10s %6s %10s %10s %10s' % ('kernel', 'grid', 'calls', 'avg_ms', 'min_ms', 'max_ms'))
     for (name, grid), d in sorted(g.items(), key=lambda kv: -sum(kv[1])):
         print('%-48s %10d %6d %10.4f %10.4f %10.4f' % (name[:48], grid, len(d), sum(d) / len(d), min(d), max(d)))
+    if a.json:
+        # bench.py's kernel names: the average over the largest-grid launches (the timed steps)
+        names = {'k_front': 'k_front', 'k_channelize': 'k_channelize', 'k_lpf_phase': 'k_lpf_phase',
+                 'k_trig_spec': 'k_trig_spec', 'k_pulse_heights': 'k_pulse_heights'}
+        best = {}
+        for (name, grid), d in g.items():
+            for key, short in names.items():
+                if key in name and (short not in best or grid > best[short][0]):
+                    best[short] = (grid, sum(d) / len(d))
+        rec = json.load(open(a.json)) if os.path.exists(a.json) else {}
+        rec['config%d' % a.config] = {k: round(v[1], 4) for k, v in best.items()}
+        rec['config%d' % a.config]['source'] = a.csv
+        json.dump(rec, open(a.json, 'w'), indent=1)
 
 
 if __name__ == '__main__':

@@ -88,6 +88,7 @@ struct mkid_ctx {
     int zi = 0;
     int64_t G = 0;  // pipeline sub-chunk (samples)
     bool fused = false;  // K1-K6 in k_front (no z buffers, no stream B work)
+    bool front_v2 = false;  // fused front end is k_front2 (N = 512..2048; MKID_FRONT_V1=1 forces v1)
     int64_t H = 0;       // ADC history samples carried between calls
     // workspace
     float2* d_zb[2] = {nullptr, nullptr};
@@ -320,6 +321,10 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->device = device;
     c->C = C; c->N = N; c->M = N / 2; c->T = kPfbTaps; c->P = P;
     c->fused = cfg->front == MKID_FRONT_AUTO && front_supported(N);
+    {
+        const char* v1 = getenv("MKID_FRONT_V1");
+        c->front_v2 = c->fused && front2_supported(N) && !(v1 && atoi(v1) != 0);
+    }
     // split front end: a large call is cut into 4 sub-chunks so the channeliser (stream A) of
     // sub-chunk i+1 overlaps the low-pass/trigger (stream B) of sub-chunk i
     int64_t G = cfg->max_chunk;
@@ -690,7 +695,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
         tstart(c, MKID_K_FRONT, &kt, s);
-        HIPCHK(c, launch_front(N, fa, s));
+        HIPCHK(c, c->front_v2 ? launch_front2(N, fa, s) : launch_front(N, fa, s));
         tstop(c, &kt, s);
         int r = run_trigger(c, c->d_raw, subs[si], stride, seg_off, capseg, s);
         if (r) return r;

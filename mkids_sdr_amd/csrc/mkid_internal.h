@@ -176,6 +176,8 @@ inline hipError_t ensure_lds_attr(std::atomic<uint64_t>& mask, const void* fn, i
 
 bool channelize_supported(int N);
 bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length
+bool front2_supported(int N);        // the one-exchange fused kernel (k_front2.hip) for this N
+hipError_t launch_front2(int N, const FrontArgs& a, hipStream_t s);
 int64_t front_hist_samples(int N);  // ADC history the fused kernel reads before a chunk
 
 }  // namespace mkid

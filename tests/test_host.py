@@ -259,3 +259,18 @@ def test_cpu_baseline_tool_runs(tmp_path):
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out['one_core']['value'] > 0 and out['all_cores']['cores'] == 2 and out['c1']['value'] > 0
     assert out['os_cpu_count'] >= 1 and out['cpu_model']
+
+
+@pytest.mark.parametrize('N', [512, 1024, 2048])
+def test_front2_index_maps_and_lds_layouts(N):
+    """k_front2.hip: the in-wave FFT staging reproduces numpy's FFT, the decimation combine of the
+    select is exact, and every LDS access pattern is bank-conflict free on gfx950."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location('front2_layouts', os.path.join(root, 'tools', 'front2_layouts.py'))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.fft_emulation() < 1e-10
+    assert m.decimation_combine(N) < 1e-9
+    ok = m.check_layouts(N)
+    assert all(ok.values()), ok

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Checks of k_front2.hip's index maps and LDS layouts (run by tests/test_host.py on the CPU).
+
+1. numpy emulation of one wave's 512-point FFT exactly as the kernel stages it (radix-8 over
+   registers, twiddle, T1 bit swaps register<->lane bits 3-5, radix-8, twiddle, T2 through LDS
+   with the i + (i >> 3) layout, radix-8): lane L, register r must end holding
+   Y[(L >> 3) + 8 (L & 7) + 64 r]; and the NW-way decimation combine of the select.
+2. gfx950 bank-conflict freedom (MI355X_MICROARCH.md §LDS) of every LDS access pattern:
+   ds_read_b32 ring reads, ds_read_b64 tap reads, ds_write_b32/b64/b128 ring writes, the
+   ds_write_b64 / ds_read_b64 T2 exchange and the ds_write_b64 Y write.
+"""
+import numpy as np
+
+
+def fft_emulation(seed=0):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(size=512) + 1j * rng.normal(size=512)
+    W = lambda n, e: np.exp(-2j * np.pi * e / n)
+    V = np.array([[x[64 * r + L] for r in range(8)] for L in range(64)])
+    dft8 = lambda V: np.fft.fft(V, axis=1)
+    V = dft8(V)
+    V *= W(512, np.outer(np.arange(64), np.arange(8)))
+    def bitswap(V, i, j):
+        U = V.copy()
+        for L in range(64):
+            for r in range(8):
+                if ((r >> i) & 1) != ((L >> j) & 1):
+                    U[L, r] = V[L ^ (1 << j), r ^ (1 << i)]
+        return U
+    for i in range(3):
+        V = bitswap(V, i, 3 + i)
+    V = dft8(V)
+    V *= W(64, np.outer(np.arange(64) & 7, np.arange(8)))
+    mem = np.zeros(576, complex)
+    f = lambda i: i + (i >> 3)
+    for L in range(64):
+        for r in range(8):
+            mem[f(64 * (L >> 3) + 8 * r + (L & 7))] = V[L, r]
+    U = np.array([[mem[f(64 * (L >> 3) + 8 * (L & 7) + r)] for r in range(8)] for L in range(64)])
+    V = dft8(U)
+    Y = np.fft.fft(x)
+    return max(abs(V[L, r] - Y[(L >> 3) + 8 * (L & 7) + 64 * r]) for L in range(64) for r in range(8))
+
+
+def decimation_combine(N, seed=1):
+    rng = np.random.default_rng(seed)
+    u = rng.normal(size=N) + 1j * rng.normal(size=N)
+    NW = N // 512
+    Ys = [np.fft.fft(u[w::NW]) for w in range(NW)]
+    k = np.arange(N)
+    X = sum(np.exp(-2j * np.pi * w * k / N) * Ys[w][k % 512] for w in range(NW))
+    return np.abs(X - np.fft.fft(u)).max()
+
+
+def _groups(width):
+    """lane groups (one LDS cycle each) and bank count of an instruction (MI355X_MICROARCH.md)."""
+    if width == 'r32':
+        return [range(0, 32), range(32, 64)], 32
+    if width == 'r64':
+        return [range(0, 32), range(32, 64)], 64
+    if width == 'w32':
+        return [range(0, 32), range(32, 64)], 32
+    if width == 'w64':
+        return [range(16 * g, 16 * g + 16) for g in range(4)], 32
+    if width == 'w128':
+        return [range(8 * g, 8 * g + 8) for g in range(8)], 32
+    raise ValueError(width)
+
+
+def conflict_free(dword_addr_of_lane, ndw, width):
+    groups, nb = _groups(width)
+    for g in groups:
+        banks = {}
+        for L in g:
+            a = dword_addr_of_lane(L)
+            for d in range(ndw):
+                b = (a + d) % nb
+                banks.setdefault(b, set()).add(a + d)
+        if any(len(s) > 1 for s in banks.values()):
+            return False
+    return True
+
+
+def check_layouts(N):
+    NW, M = N // 512, N // 2
+    Q = M // NW
+    ok = {}
+    # ring reads: point NW (64 r + L) + w at w Q + 64 (r & 3) + L (4-byte samples)
+    ok['ring_read'] = all(conflict_free(lambda L, w=w, r=r: w * Q + 64 * (r & 3) + L, 1, 'r32')
+                          for w in range(NW) for r in range(8))
+    ok['tap_read'] = all(conflict_free(lambda L, w=w, r=r: 2 * (w * 512 + 64 * r + L), 2, 'r64')
+                         for w in range(NW) for r in range(8))
+    # ring writes: thread t writes samples 4t'..4t'+3 (t' = t mod M/4) of one hop
+    if NW == 4:
+        ok['ring_write'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')
+                               for j in range(4) for b in range(0, M // 4, 64))
+    elif NW == 2:
+        ok['ring_write'] = all(conflict_free(lambda L, j=j, b=b: j * Q + 2 * (b + L), 2, 'w64')
+                               for j in range(2) for b in range(0, M // 4, 64))
+    else:
+        ok['ring_write'] = all(conflict_free(lambda L, b=b: 4 * (b + L), 4, 'w128') for b in range(0, M // 4, 64))
+    f = lambda i: i + (i >> 3)
+    ok['t2_write'] = all(conflict_free(lambda L, r=r: 2 * f(64 * (L >> 3) + 8 * r + (L & 7)), 2, 'w64')
+                         for r in range(8))
+    ok['t2_read'] = all(conflict_free(lambda L, r=r: 2 * f(64 * (L >> 3) + 8 * (L & 7) + r), 2, 'r64')
+                        for r in range(8))
+    g = lambda k: k ^ ((k >> 2) & 14)
+    ok['y_write'] = all(conflict_free(lambda L, r=r: 2 * g((L >> 3) + 8 * (L & 7) + 64 * r), 2, 'w64')
+                        for r in range(8))
+    ok['y_bijective'] = len({g(k) for k in range(512)}) == 512 and max(g(k) for k in range(512)) < 576
+    ok['t2_fits'] = max(f(i) for i in range(512)) < 576
+    return ok
+
+
+if __name__ == '__main__':
+    print('fft emulation max error', fft_emulation())
+    for N in (512, 1024, 2048):
+        print(N, 'combine error', decimation_combine(N), check_layouts(N))

@@ -26,18 +26,20 @@ def main():
         grid = int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) * int(r['Grid_Size_Z'])
         name = r['Kernel_Name'].split('(')[0]
         g[(name, grid)].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6)
-    print('%-48s %10s %6s %10s %10s %10s' % ('kernel', 'grid', 'calls', 'avg_ms', 'min_ms', 'max_ms'))
+    print('%-48s %10s %6s %10s %10s %10s %10s' % ('kernel', 'grid', 'calls', 'avg_ms', 'median_ms', 'min_ms', 'max_ms'))
+    med = lambda d: sorted(d)[len(d) // 2]
     for (name, grid), d in sorted(g.items(), key=lambda kv: -sum(kv[1])):
-        print('%-48s %10d %6d %10.4f %10.4f %10.4f' % (name[:48], grid, len(d), sum(d) / len(d), min(d), max(d)))
+        print('%-48s %10d %6d %10.4f %10.4f %10.4f %10.4f' % (name[:48], grid, len(d), sum(d) / len(d), med(d), min(d),
+                                                             max(d)))
     if a.json:
-        # bench.py's kernel names: the average over the largest-grid launches (the timed steps)
+        # bench.py's kernel names: the median over the largest-grid launches (the timed steps)
         names = {'k_front': 'k_front', 'k_channelize': 'k_channelize', 'k_lpf_phase': 'k_lpf_phase',
                  'k_trig_spec': 'k_trig_spec', 'k_pulse_heights': 'k_pulse_heights'}
         best = {}
         for (name, grid), d in g.items():
             for key, short in names.items():
                 if key in name and (short not in best or grid > best[short][0]):
-                    best[short] = (grid, sum(d) / len(d))
+                    best[short] = (grid, med(d))   # median: the cold first launch is an outlier
         rec = json.load(open(a.json)) if os.path.exists(a.json) else {}
         rec['config%d' % a.config] = {k: round(v[1], 4) for k, v in best.items()}
         rec['config%d' % a.config]['source'] = a.csv

@@ -28,7 +28,7 @@ import struct
 
 import numpy as np
 
-from . import codecs, lut
+from . import codecs, lut, packets
 
 FIR_RE = re.compile(r'^FIR_b(\d+)b(\d+)$')
 PULSE_RING = 2 ** 14          # pulses_bram0/1 depth (ROACH_Pulses.py:799-800)
@@ -71,9 +71,14 @@ class FpgaClient:
         self.rng = np.random.default_rng(seed)
         self._chan = None
         self._t = 0                      # loop-back source position (ADC samples)
-        self._ring = np.zeros(PULSE_RING, np.uint64)
-        self._addr = 0
+        self._j = 0                      # phase rows the device stream has processed since reset
+        # photon-packet wire path (packets.py): time-ordered words with us-since-PPS stamps and
+        # end-of-second markers into the pulses_bram0/1 ring while startBuffer is 1
+        self._wire = packets.WireStream(sample_rate, self.N)
+        self.ring = packets.PulseRing()
         self._buffering = False
+        self.pulse_rows = 4096           # phase rows streamed between two pulses_addr reads
+        self.packet_log = None           # a list to record (wide packets, j0, rows) per call
         self.boffile = None
 
     # ---- katcp surface -----------------------------------------------------------------------
@@ -84,6 +89,9 @@ class FpgaClient:
         self._t = 0
         if self._chan is not None:
             self._chan.reset()
+        self._j = 0
+        self._wire = packets.WireStream(self.fs, self.N)
+        self.ring = packets.PulseRing()
         return 'ok'
 
     def is_connected(self):
@@ -123,7 +131,8 @@ class FpgaClient:
             self.cfg.baseline[key] = value
             self.cfg.dirty.add('baseline')
         elif name == 'startBuffer':
-            self._buffering = bool(value)
+            self.ring.start_buffer(value & 1, prev & 1)
+            self._buffering = bool(value & 1)
         elif name == 'conv_phase_ch_we_IQ' and self._chan is not None:
             self._chan.set_iq_tap(value)
         elif name in ('startAccumulator', 'startSnap', 'startDAC', 'avgIQ_ctrl', 'snapPhase_ctrl',
@@ -137,7 +146,7 @@ class FpgaClient:
             return 0                      # the device LUT is valid as soon as it is written
         if name == 'pulses_addr':
             self._advance_pulses()
-            return self._addr
+            return self.ring.addr
         if name not in self.regs:
             raise RuntimeError('Request read_int failed: no register named %s' % name)
         return self.regs[name]
@@ -177,9 +186,7 @@ class FpgaClient:
             I, Q = self._iq_of(self.regs.get('conv_phase_ch_we_IQ', 0), size // 8)
             return codecs.encode_iq_snap(I, Q)[:size]
         if name in ('pulses_bram0', 'pulses_bram1'):
-            w0, w1 = codecs.reference_bram_words(self._ring)
-            w = w0 if name == 'pulses_bram0' else w1
-            return w.astype('>u4').tobytes()[offset:offset + size]
+            return self.ring.read(name, size, offset)
         if name in self.regs and isinstance(self.regs[name], bytes):
             return self.regs[name][offset:offset + size]
         raise RuntimeError('Request read failed: no readable register named %s' % name)
@@ -223,15 +230,27 @@ class FpgaClient:
         self._t += n
         return np.clip(np.trunc(x), -32768, 32767).astype(np.int16)
 
+    def _process(self, ch, n_phase_samples):
+        """One device call over the next loop-back samples. Like the firmware, the packet stage
+        feeds the pulses ring whenever startBuffer is 1, whatever the call was made for."""
+        j0 = self._j
+        phase, ev = ch.process(self.adc(n_phase_samples * self.N))
+        self._j += n_phase_samples
+        if self.packet_log is not None:       # test hook: every call's device packets
+            self.packet_log.append((ev, j0, n_phase_samples))
+        words = self._wire.push(ev, j0, n_phase_samples)
+        if self._buffering and len(words):
+            self.ring.write(words)
+        return phase, ev
+
     def run(self, n_phase_samples):
         """Stream enough loop-back ADC data for n phase samples per channel; returns
         (phase [n][C], wide packets)."""
-        ch = self.sync()
-        return ch.process(self.adc(n_phase_samples * self.N))
+        return self._process(self.sync(), n_phase_samples)
 
     def _read_avgiq(self, size):
         ch = self.sync()
-        ch.process(self.adc(256 * self.N))       # accumulate over 256 phase samples
+        self._process(ch, 256)                   # accumulate over 256 phase samples
         mi, mq = ch.avg_iq()
         words = np.concatenate([np.rint(mi), np.rint(mq)]).astype('>i4')
         return words.tobytes()[:size]
@@ -251,7 +270,7 @@ class FpgaClient:
         left = npairs
         while left > 0:
             n = min(step, left)
-            c.process(self.adc(n * self.N))
+            self._process(c, n)
             out.append(c.iq_tap())
             left -= n
         iq = np.concatenate(out).astype(np.int64) if out else np.zeros((0, 2), np.int64)
@@ -265,15 +284,9 @@ class FpgaClient:
         return codecs.encode_snap_phase(raw)[:size]
 
     def _advance_pulses(self):
-        if not self._buffering:
-            return
-        _, ev = self.run(4096)
-        if len(ev) == 0:
-            return
-        ref = codecs.wide_to_reference(ev[codecs.unpack_wide(ev)['ch'] < 255])
-        for w in ref:
-            self._ring[self._addr] = w
-            self._addr = (self._addr + 1) % PULSE_RING
+        """Time passes between two reads of pulses_addr: stream pulse_rows more phase rows."""
+        if self._buffering:
+            self.run(self.pulse_rows)
 
 
 def _s32(v):

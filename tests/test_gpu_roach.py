@@ -91,3 +91,72 @@ def test_snapshot_registers_readback(gpu):
     q = roach.read('qdr0_memory', 4 * 1024)
     vals = struct.unpack('>%dh' % 2048, q)                     # ROACH_Pulses.py:471
     assert len(vals) == 2048 and np.abs(np.median(vals)) < 1000
+
+
+def test_pulse_ring_packetmaster_seconds(gpu):
+    """§8(f)1 end to end: the device trigger feeds the firmware wire stream (us since PPS,
+    end-of-second markers) into the pulses ring while startBuffer is 1; PulseServer ships the
+    ring halves (PulseServer.c:151-227, 318-386) and PacketMaster bins them per pixel per second
+    (PacketMaster.c:304-397, 978-1023). Over >= 2 simulated seconds the binned rows equal the
+    per-packet restatement (oracle/packet_ref.py) fed with the device's own packets."""
+    from mkids_sdr_amd import packets
+    from oracle import packet_ref
+    C, fs = 64, 1 << 21                      # 16384 phase rows per second
+    N = 2 * C
+    roach = FpgaClient(n_channels=C, sample_rate=fs, noise_sigma=40.0, seed=11)
+    roach.progdev('pulse_trigger_2022_Jan_24_1322.bof')
+    roach.packet_log = []
+    freqs = list(4.0e9 + np.array([-29, -21, -13, -6, 3, 9, 17, 26]) * (fs / N))
+    rs = RoachSetup(roach, freqs, 4.0e9, n_channels=C, sample_rate=fs)
+    rs.define_LUTs()
+    rs.toggleDAC()
+    rs.rotateLoopsReady()
+    rp = RoachPulses(roach, len(freqs), np.loadtxt(os.path.join(GOLD, 'fir', 'matched_30us.txt')),
+                     n_channels=C)
+    rp.loadFIRcoeffs()
+    rp.customThresholds[:len(freqs)] = 0.0   # threshold at the baseline: noise triggers often
+    rp.loadThresholds()
+
+    roach.write_int('startBuffer', 0)        # PulseServer.c:78-80
+    roach.write_int('startBuffer', 1)
+    k0 = roach._wire.next_sec                # first second the ring will carry in full
+    server = packets.PulseServer(roach.ring)
+    pm = packets.PacketMaster(1, C, exptime=2, dataset='t0')
+    sent = []
+    for _ in range(64):
+        roach.read_int('pulses_addr')        # time passes: pulse_rows more phase rows
+        blk = server.poll()
+        if blk is not None:
+            sent.append(blk)
+            pm.receive(0, *blk)
+        if pm.done():
+            break
+    roach.write_int('startBuffer', 0)
+    assert pm.done() and pm.corrupted_eos == 0 and pm.nonpixel == 0
+    assert pm.photon_counts[:, :len(freqs)].min() > 50         # every tone channel, both seconds
+    assert pm.photon_counts[:, len(freqs):].max() == 0         # deleted channels stay silent
+
+    # the restatement over the device's own packets
+    truth = []
+    for ev, j0, n in roach.packet_log:
+        f = codecs.unpack_wide(ev)
+        rows = j0 - 1 + ((f['ts'] - (j0 - 1)) % (1 << 28))
+        truth += list(zip(rows.tolist(), f['ch'].tolist(), f['peak'].tolist(), f['base'].tolist()))
+    words = packet_ref.wire_stream(truth, fs, N, roach._j)
+    eos = [i for i, w in enumerate(words) if w == packet_ref.EOS]
+    words = words[eos[k0 - 1] + 1:] if k0 > 0 else words
+    ref_sent = packet_ref.pulse_server(words)
+    assert len(ref_sent) >= len(sent)
+    for (lo, hi), (rlo, rhi) in zip(sent, ref_sent):
+        assert [int(x) for x in np.frombuffer(lo, '>u4')] == rlo
+        assert [int(x) for x in np.frombuffer(hi, '>u4')] == rhi
+    rows, counts, _, _ = packet_ref.packet_master(ref_sent[:len(sent)], C, 2)
+    assert np.array_equal(pm.photon_counts, np.array(counts))
+    for p in range(len(freqs)):
+        for s in range(2):
+            assert [int(x) for x in pm.rows[(0, p)][s]] == rows[p][s]
+            us = packets.decode_wire(pm.rows[(0, p)][s])['us']
+            assert np.all(np.diff(us) > 0) and us.max() < 10 ** 6
+    # the reference readPulses decodes the same ring (EOS words appear as channel 255)
+    got = rp.readPulses(steps=1)
+    assert set(got) <= set(range(len(freqs))) | {255}

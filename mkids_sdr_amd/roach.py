@@ -79,6 +79,10 @@ class FpgaClient:
         self._buffering = False
         self.pulse_rows = 4096           # phase rows streamed between two pulses_addr reads
         self.packet_log = None           # a list to record (wide packets, j0, rows) per call
+        self.lo = None                   # current LO (set_lo); None = nominal
+        self.lo_nominal = None
+        self.resonators = []             # RESDIFF parameter dicts (set_resonators)
+        self._adc_cache = None
         self.boffile = None
 
     # ---- katcp surface -----------------------------------------------------------------------
@@ -92,6 +96,7 @@ class FpgaClient:
         self._j = 0
         self._wire = packets.WireStream(self.fs, self.N)
         self.ring = packets.PulseRing()
+        self._adc_cache = None
         return 'ok'
 
     def is_connected(self):
@@ -160,6 +165,7 @@ class FpgaClient:
                                                                   self.cfg.dds_lag)
             self.cfg.dirty.add('dds')
             self._t = 0
+            self._adc_cache = None
             return None
         m = FIR_RE.match(name)
         if m:
@@ -221,10 +227,49 @@ class FpgaClient:
         d.dirty.clear()
         return ch
 
+    # ---- loop-back source with resonators ---------------------------------
+    def set_lo(self, freq):
+        """The LO synthesiser (programLOrev2board's ADF4355 SPI writes, ROACH_Setup.py:307-393,
+        are control plane): DAC and ADC share it, so moving it moves every tone across its
+        resonator while the baseband comb, and so every channel, stays put."""
+        self.lo = float(freq)
+        self._adc_cache = None
+
+    def set_resonators(self, resonators, lo_nominal):
+        """Put MKID resonators on the feedline: a list of dicts of iqsweep.RESDIFF parameters
+        (lib/iqsweep.py:824-858: Q, f0, aleak, ph1, da, ang1, Igain, Qgain, Ioff, Qoff). Each DAC
+        comb bin passes the resonator whose f0 is nearest its RF frequency at lo_nominal, with
+        the complex transmission RESDIFF gives at its RF frequency for the current LO."""
+        self.resonators = [dict(r) for r in resonators]
+        self.lo_nominal = float(lo_nominal)
+        if self.lo is None:
+            self.lo = self.lo_nominal
+        self._adc_cache = None
+
+    def _adc_lut(self):
+        """One 2^16-sample period of the loop-back ADC stream, complex float64: conj(DAC LUT)
+        (ROACH_Setup.py:485-487), each comb bin times its resonator's transmission."""
+        if self._adc_cache is None:
+            x = self.cfg.dac_i.astype(np.float64) - 1j * self.cfg.dac_q.astype(np.float64)
+            if self.resonators:
+                X = np.fft.fft(x)
+                fbb = np.fft.fftfreq(lut.LUT_LEN, 1.0 / self.fs)
+                f0 = np.array([r['f0'] for r in self.resonators])
+                which = np.argmin(np.abs((self.lo_nominal + fbb)[:, None] - f0[None, :]), axis=1)
+                H = np.empty(lut.LUT_LEN, complex)
+                for m, r in enumerate(self.resonators):
+                    sel = which == m
+                    H[sel] = resdiff(self.lo + fbb[sel], **r)
+                x = np.fft.ifft(X * H)
+            self._adc_cache = x
+        return self._adc_cache
+
     def adc(self, n):
-        """Next n loop-back ADC samples: conj(DAC LUT) tiled (+ optional AWGN), int16 [n][2]."""
+        """Next n loop-back ADC samples: conj(DAC LUT) through the resonators, tiled (+ optional
+        AWGN), int16 [n][2]."""
         idx = (self._t + np.arange(n)) % lut.LUT_LEN
-        x = np.stack([self.cfg.dac_i[idx], -self.cfg.dac_q[idx]], axis=1).astype(np.float64)
+        z = self._adc_lut()[idx]
+        x = np.stack([z.real, z.imag], axis=1)
         if self.noise_sigma > 0:
             x += self.rng.normal(0, self.noise_sigma, x.shape)
         self._t += n
@@ -250,6 +295,7 @@ class FpgaClient:
 
     def _read_avgiq(self, size):
         ch = self.sync()
+        self._process(ch, 64)                    # settle: filters forget the previous LO / LUTs
         self._process(ch, 256)                   # accumulate over 256 phase samples
         mi, mq = ch.avg_iq()
         words = np.concatenate([np.rint(mi), np.rint(mq)]).astype('>i4')
@@ -287,6 +333,19 @@ class FpgaClient:
         """Time passes between two reads of pulses_addr: stream pulse_rows more phase rows."""
         if self._buffering:
             self.run(self.pulse_rows)
+
+
+def resdiff(x, Q, f0, aleak=0.0, ph1=0.0, da=0.0, ang1=0.0, Igain=1.0, Qgain=1.0, Ioff=0.0, Qoff=0.0):
+    """iqsweep.RESDIFF (lib/iqsweep.py:824-858), vectorised: the resonator IQ loop model at
+    frequencies x, returned as complex nI + i nQ (the reference returns [nI, nQ] stacked)."""
+    dx = (np.asarray(x, np.float64) - f0) / f0
+    j2 = 2.0j * Q * dx
+    s21b = da * dx + (j2 / (1.0 + j2) - 0.5) + aleak * ((1.0 - np.cos(dx * ph1)) - 1j * np.sin(dx * ph1))
+    Ix1 = s21b.real * Igain
+    Qx1 = s21b.imag * Qgain
+    nI = Ix1 * np.cos(ang1) + Qx1 * np.sin(ang1) + Ioff
+    nQ = -Ix1 * np.sin(ang1) + Qx1 * np.cos(ang1) + Qoff
+    return nI + 1j * nQ
 
 
 def _s32(v):
@@ -382,16 +441,50 @@ class RoachSetup:
         v = np.frombuffer(data, '>i4').astype(np.float64)
         return v[:self.n_channels], v[self.n_channels:]
 
-    def rotateLoopsReady(self):
+    def rotateLoopsReady(self, sweep=None):
         """ROACH_Setup.py:645-671 for every tone channel: DDS phase = arctan2 of the on-resonance
-        average IQ (centre-subtracted), then redefine + rewrite the LUTs."""
+        average IQ (centre-subtracted), then redefine + rewrite the LUTs; sweep = (loSpan, steps)
+        re-sweeps the loops afterwards as the reference does (sweepLO, :671)."""
         I, Q = self.read_avg_iq()
         phase = [0.] * self.n_channels
         for n in range(len(self.dac_freqs)):
             phase[n] = np.arctan2(Q[n] - self.iq_centers[n].imag, I[n] - self.iq_centers[n].real)
         self.define_DDS_LUT(phase)
         self.write_LUTs()
+        if sweep is not None:        # :670-671 re-sweeps, so the centres follow the rotation
+            self.sweepLOready(*sweep)
         return phase
+
+    def programLOrev2board(self, freq=3.2e9, sweep_freq=0, enable=1):
+        """ROACH_Setup.py:307-393: the LO at freq (sweep_freq) or at the LO spin box value; the
+        ADF4355 register words themselves are control plane (FpgaClient.set_lo)."""
+        self.roach.set_lo(freq if sweep_freq else self.lo_freq)
+
+    def sweepLOready(self, loSpan, steps):
+        """ROACH_Setup.py:699-810 at one attenuation: step the LO over loSpan in `steps` steps
+        (lo_freqs :724), read avgIQ at each step (:767-782), return to the LO (:783), read the
+        on-resonance avgIQ and set each tone's IQ centre to the middle of its swept loop
+        (findIQcenters, :786-796), and the IQ velocities (:805-810). Returns (I, Q) [N_freqs][steps]."""
+        self.N_freqs = len(self.dac_freqs)
+        f_base = self.lo_freq
+        df = loSpan / steps
+        lo_freqs = [f_base + i * df - 0.5 * steps * df for i in range(steps)]
+        self.f_span = [[f - 0.5 * steps * df + n * df for n in range(steps)] for f in self.dac_freqs]
+        I = np.zeros((self.N_freqs, steps))
+        Q = np.zeros((self.N_freqs, steps))
+        for i in range(steps):
+            self.programLOrev2board(lo_freqs[i], 1)
+            Ia, Qa = self.read_avg_iq()
+            I[:, i] = Ia[:self.N_freqs]
+            Q[:, i] = Qa[:self.N_freqs]
+        self.programLOrev2board(f_base, 1)
+        Ia, Qa = self.read_avg_iq()
+        self.I_on_res, self.Q_on_res = list(Ia[:self.N_freqs]), list(Qa[:self.N_freqs])
+        for j in range(self.N_freqs):
+            self.iq_centers[j] = self.findIQcenters(I[j], Q[j])
+        self.IQ_vels = np.hypot(np.diff(I, axis=1), np.diff(Q, axis=1))
+        self.I, self.Q = I, Q
+        return I, Q
 
 
 class RoachPulses:

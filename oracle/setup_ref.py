@@ -281,3 +281,24 @@ def decode_pulses(bram0, bram1, addr0, addr1, n_words=2 ** 14):
         for n in range(0, addr1):
             one(n, True)
     return out
+
+
+def resdiff(x, Q, f0, aleak, ph1, da, ang1, Igain, Qgain, Ioff, Qoff):
+    """lib/iqsweep.py:824-858 RESDIFF, element by element (np.vectorize(complex) as written)."""
+    x = np.asarray(x, dtype=float)
+    l = len(x)
+    dx = (x - f0) / f0
+    s21a = (np.vectorize(complex)(0, 2.0 * Q * dx)) / (complex(1, 0) + np.vectorize(complex)(0, 2.0 * Q * dx))
+    s21a = s21a - complex(.5, 0)
+    s21b = np.vectorize(complex)(da * dx, 0) + s21a + aleak * np.vectorize(complex)(1.0 - np.cos(dx * ph1),
+                                                                                   -np.sin(dx * ph1))
+    Ix1 = s21b.real * Igain
+    Qx1 = s21b.imag * Qgain
+    nI1 = Ix1 * np.cos(ang1) + Qx1 * np.sin(ang1)
+    nQ1 = -Ix1 * np.sin(ang1) + Qx1 * np.cos(ang1)
+    nI1 = nI1 + Ioff
+    nQ1 = nQ1 + Qoff
+    s21 = np.zeros(l * 2)
+    s21[:l] = nI1
+    s21[l:] = nQ1
+    return s21

@@ -103,7 +103,7 @@ def test_pulse_ring_packetmaster_seconds(gpu):
     from oracle import packet_ref
     C, fs = 64, 1 << 21                      # 16384 phase rows per second
     N = 2 * C
-    roach = FpgaClient(n_channels=C, sample_rate=fs, noise_sigma=40.0, seed=11)
+    roach = FpgaClient(n_channels=C, sample_rate=fs, noise_sigma=600.0, seed=11)
     roach.progdev('pulse_trigger_2022_Jan_24_1322.bof')
     roach.packet_log = []
     freqs = list(4.0e9 + np.array([-29, -21, -13, -6, 3, 9, 17, 26]) * (fs / N))
@@ -132,7 +132,9 @@ def test_pulse_ring_packetmaster_seconds(gpu):
         if pm.done():
             break
     roach.write_int('startBuffer', 0)
-    assert pm.done() and pm.corrupted_eos == 0 and pm.nonpixel == 0
+    diag = dict(written=roach.ring.written, halves=len(sent), sec=pm.sec, rows=roach._j, k0=k0,
+                thr=roach.cfg.thr[:len(freqs)].tolist(), packets=sum(len(e) for e, _, _ in roach.packet_log))
+    assert pm.done() and pm.corrupted_eos == 0 and pm.nonpixel == 0, diag
     assert pm.photon_counts[:, :len(freqs)].min() > 50         # every tone channel, both seconds
     assert pm.photon_counts[:, len(freqs):].max() == 0         # deleted channels stay silent
 
@@ -160,3 +162,55 @@ def test_pulse_ring_packetmaster_seconds(gpu):
     # the reference readPulses decodes the same ring (EOS words appear as channel 255)
     got = rp.readPulses(steps=1)
     assert set(got) <= set(range(len(freqs))) | {255}
+
+
+def test_lo_sweep_loop_calibration(gpu):
+    """§8(f)3: resonator IQ loops (iqsweep.RESDIFF) on the loop-back feedline; sweepLOready
+    (ROACH_Setup.py:699-810) steps the LO and reads the device avgIQ at each step, findIQcenters
+    puts each centre in the middle of its swept loop, loadIQcenters loads it, and
+    rotateLoopsReady (:645-671, re-sweeping as the reference does) rotates every loop so the
+    on-resonance phase is 0. The synthetic loop centre in channel units is K (Ioff + i Qoff),
+    K = the chain's response to the tone with the resonators off; radius 0.5 |K|."""
+    C, fs, lo = 64, 128e6, 4.0e9
+    roach = FpgaClient(n_channels=C, sample_rate=fs, noise_sigma=4.0, seed=8)
+    roach.progdev('pulse_trigger_2022_Jan_24_1322.bof')
+    res_hz = fs / 2 ** 16
+    offs = np.array([-40e6, -12e6, 21e6, 50e6])
+    freqs = list(lo + np.round(offs / res_hz) * res_hz)
+    rs = RoachSetup(roach, freqs, lo, n_channels=C, sample_rate=fs)
+    rng = np.random.default_rng(2)
+    res = [dict(Q=2.0e4, f0=f + 20e3, ang1=float(rng.uniform(-3, 3)), Ioff=float(rng.uniform(-.3, .3)),
+                Qoff=float(rng.uniform(-.3, .3))) for f in freqs]
+    rs.define_LUTs()
+    rs.toggleDAC()
+    rs.programLOrev2board(lo, 0)
+
+    def chain_gain():
+        roach.set_resonators([], lo)
+        I, Q = rs.read_avg_iq()
+        roach.set_resonators(res, lo)
+        return (I + 1j * Q)[:len(freqs)]
+
+    def check_centres(K):
+        want = K * np.array([r['Ioff'] + 1j * r['Qoff'] for r in res])
+        err = np.abs(rs.iq_centers[:len(freqs)] - want) / (0.5 * np.abs(K))
+        assert np.all(np.abs(K) > 300), K
+        assert err.max() < 0.01, err
+
+    K = chain_gain()
+    span, steps = 1.2e6, 120                  # +-3 linewidths (f0/Q = 200 kHz), 10 kHz steps
+    I, Q = rs.sweepLOready(span, steps)
+    assert I.shape == (len(freqs), steps) and rs.IQ_vels.shape == (len(freqs), steps - 1)
+    check_centres(K)
+    # the sweep traces a circle of radius 0.5 |K| about the centre
+    r = np.abs(I + 1j * Q - rs.iq_centers[:len(freqs), None])
+    assert np.all(np.abs(r / (0.5 * np.abs(K)[:, None]) - 1) < 0.03), r
+    rs.loadIQcenters()
+    assert np.allclose(roach.cfg.ic[:len(freqs)], rs.iq_centers[:len(freqs)].real, atol=8)
+
+    rs.rotateLoopsReady(sweep=(span, steps))  # DDS rotated, loops re-swept in the new frame
+    check_centres(chain_gain())
+    rs.loadIQcenters()
+    phase, _ = roach.run(2048)
+    tone_phase = np.angle(np.exp(1j * phase[64:, :len(freqs)]).mean(0))
+    assert np.abs(tone_phase).max() < 0.05, tone_phase

@@ -274,3 +274,41 @@ def test_front2_index_maps_and_lds_layouts(N):
     assert m.decimation_combine(N) < 1e-9
     ok = m.check_layouts(N)
     assert all(ok.values()), ok
+
+
+def test_resdiff_matches_reference_restatement():
+    """The shim's vectorised resonator model equals iqsweep.RESDIFF (lib/iqsweep.py:824-858)."""
+    from mkids_sdr_amd.roach import resdiff
+    from oracle import setup_ref
+    f = np.linspace(3.999e9, 4.001e9, 257)
+    p = dict(Q=2.3e4, f0=4.0001e9, aleak=0.3, ph1=1.7e3, da=-0.2, ang1=0.7, Igain=1.1, Qgain=0.9,
+             Ioff=0.05, Qoff=-0.12)
+    ref = setup_ref.resdiff(f, **p)
+    got = resdiff(f, **p)
+    assert np.allclose(got.real, ref[:257], rtol=0, atol=1e-12)
+    assert np.allclose(got.imag, ref[257:], rtol=0, atol=1e-12)
+
+
+def test_loopback_resonator_source():
+    """FpgaClient's loop-back source with resonators: a single DAC tone comes back multiplied by
+    the resonator's complex transmission at the tone's RF frequency for the current LO."""
+    from mkids_sdr_amd import lut
+    from mkids_sdr_amd.roach import FpgaClient, resdiff
+    fs, C, lo = 128e6, 64, 4.0e9
+    roach = FpgaClient(n_channels=C, sample_rate=fs, gpu=False)
+    f_rf = lo + 21 * fs / lut.LUT_LEN * 64
+    I, Q, freqs, sf, ph = lut.define_dac_lut([f_rf], lo, np.zeros(1), fs)
+    roach.cfg.dac_i, roach.cfg.dac_q = I, Q
+    plain = roach._adc_lut().copy()
+    r = dict(Q=1e4, f0=f_rf + 2e5, ang1=0.3, Ioff=0.1, Qoff=0.05)
+    roach.set_resonators([r], lo)
+    for lo_now in (lo, lo - 3e5, lo + 7e5):
+        roach.set_lo(lo_now)
+        h = resdiff(np.array([f_rf + (lo_now - lo)]), **r)[0]
+        got = np.fft.fft(roach._adc_lut())
+        ref = np.fft.fft(plain)
+        k = int(np.argmax(np.abs(ref)))                 # the tone's bin: f_rf - lo at baseband
+        assert abs(np.fft.fftfreq(lut.LUT_LEN, 1 / fs)[k] - (f_rf - lo)) < 1.0
+        assert abs(got[k] - ref[k] * h) < 1e-9 * abs(ref[k])
+        # the rest is the LUT's quantisation noise (each bin through its own transmission)
+        assert np.abs(roach._adc_lut() - plain * h).max() < 0.01 * np.abs(plain).max()

@@ -342,14 +342,14 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
                     acc[m].y = fmaf(a.taps.g[2 * m + 1], z.y, acc[m].y);
                 }
             } else {
+                // output frame: the accumulate and the shift to the next output are one FMA per
+                // accumulator (acc[m] <- acc[m+1] + g_{2m+2} z), no register moves
+                const float2 y = make_float2(fmaf(a.taps.g[0], z.x, acc[0].x), fmaf(a.taps.g[0], z.y, acc[0].y));
 #pragma unroll
-                for (int m = 0; m < 13; ++m) {
-                    acc[m].x = fmaf(a.taps.g[2 * m], z.x, acc[m].x);
-                    acc[m].y = fmaf(a.taps.g[2 * m], z.y, acc[m].y);
+                for (int m = 0; m < 12; ++m) {
+                    acc[m].x = fmaf(a.taps.g[2 * m + 2], z.x, acc[m + 1].x);
+                    acc[m].y = fmaf(a.taps.g[2 * m + 2], z.y, acc[m + 1].y);
                 }
-                const float2 y = acc[0];
-#pragma unroll
-                for (int m = 0; m < 12; ++m) acc[m] = acc[m + 1];
                 acc[12] = make_float2(0.f, 0.f);
                 if (kf > 0 && kf < nrun) {
                     const int jr = (kf - 1) >> 1;

@@ -16,7 +16,7 @@
 //
 // The result is bit-identical to the sequential oracle/trigger.c for every input; the speculation
 // only decides how much sequential work the fix-up does (EMA merges within ~10^2 samples on noisy
-// phase). SVF mode (slow 2-pole baseline with a wide dead band) runs as one exact segment.
+// phase; the slow SVF baseline needs ~10^4, so its segments warm up over kSvfW, mkid_api.hip).
 // The 26-tap matched filter uses 24-bit multiply-adds (taps are 12-bit, samples 16-bit).
 #include "trig_common.h"
 
@@ -120,9 +120,10 @@ __device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, u
     }
 }
 
-// The per-sample recurrence of k_trig_spec: trig_update itself for SVF (a single exact segment),
-// the code-state form trig_update_fast for EMA / no baseline (the throughput path).
-template <int MODE, bool FAST = (MODE != MKID_BASE_SVF)>
+// The per-sample recurrence of k_trig_spec: the code-state forms trig_update_fast (EMA / no
+// baseline) and trig_update_svf (SVF) on the throughput path, trig_update itself (FAST = false)
+// for a segment that starts in the start-of-stream hold-off.
+template <int MODE, bool FAST = true>
 struct Stepper {
     TrigState st;
     TrigCfg k;
@@ -144,6 +145,22 @@ struct Stepper<MODE, true> {
     __device__ __forceinline__ TrigState state() const { return from_fast(fs); }
 };
 
+template <>
+struct Stepper<MKID_BASE_SVF, true> {
+    FastSvf fs;
+    FastCfg q;
+    int32_t kf, kq;
+    __device__ Stepper(const TrigState& s, const TrigCfg& k, int32_t f0)
+        : fs(to_fast_svf(s)), q(fast_cfg(k)), kf(k.kf), kq(k.kq) {
+        if (!s.binit) {   // trig_update's baseline initialisation on the first sample
+            fs.low = (int64_t)f0 << 16;
+            fs.band = 0;
+        }
+    }
+    __device__ __forceinline__ bool step(int32_t f, EvInfo& ev) { return trig_update_svf(fs, f, q, kf, kq, ev); }
+    __device__ __forceinline__ TrigState state() const { return from_fast_svf(fs); }
+};
+
 template <int MODE>
 __global__ __launch_bounds__(kSpecThreads, 3) void k_trig_spec(TrigSpecArgs a) {
     const int64_t g = (int64_t)blockIdx.x * kSpecThreads + threadIdx.x;
@@ -157,7 +174,9 @@ __global__ __launch_bounds__(kSpecThreads, 3) void k_trig_spec(TrigSpecArgs a) {
     const TrigCfg k{a.thr[c], MODE, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
     const int64_t seg0 = (int64_t)s * a.L;
     const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
-    const int64_t jw = s == 0 ? 0 : seg0 - a.W;
+    // a segment closer than W to the sub-chunk start warms up from row 0 with the carried state
+    // (exact); L and W are multiples of 26 whenever W > 0, so seg0 - jw is too
+    const int64_t jw = (s == 0 || seg0 <= a.W) ? 0 : seg0 - a.W;
     QWin win;
     load_qwin(win, a, c, jw);
     const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
@@ -170,7 +189,7 @@ __global__ __launch_bounds__(kSpecThreads, 3) void k_trig_spec(TrigSpecArgs a) {
     auto rload = [&](uint32_t off) { return *reinterpret_cast<const uint32_t*>(rbase + off); };
     QWin w0 = win;
     const int32_t f0 = mf_q(w0, tp, 0, rload(roff));
-    const TrigState st0 = s == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
+    const TrigState st0 = jw == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
     auto body = [&](auto& sp) {
         // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0
         run_groups(__builtin_amdgcn_readfirstlane((int32_t)(seg0 - jw) / kFirTaps), rbase, roff, (uint32_t)(2 * C),
@@ -205,14 +224,9 @@ __global__ __launch_bounds__(kSpecThreads, 3) void k_trig_spec(TrigSpecArgs a) {
         }
         a.s_end[(int64_t)s * C + c] = sp.state();
     };
-    if constexpr (MODE != MKID_BASE_SVF) {
-        if (in_holdoff(st0)) {  // first segment after a reset: the generic recurrence
-            Stepper<MODE, false> sp(st0, k, f0);
-            body(sp);
-        } else {
-            Stepper<MODE> sp(st0, k, f0);
-            body(sp);
-        }
+    if (in_holdoff(st0)) {  // first segment after a reset: the generic recurrence
+        Stepper<MODE, false> sp(st0, k, f0);
+        body(sp);
     } else {
         Stepper<MODE> sp(st0, k, f0);
         body(sp);

@@ -34,7 +34,7 @@ struct KTime {
 
 // Speculative trigger segmentation (k_trigger.hip): segments of at least kSegL phase samples,
 // each speculating from kSegW samples of warm-up. The EMA baseline (alpha 41/512) forgets its
-// start in ~10^2 samples on noisy phase; SVF runs as a single exact segment. A long call uses
+// start in ~10^2 samples on noisy phase (SVF: see kSvfW below). A long call uses
 // longer segments so that the (channel, segment) waves fit the GPU's resident wave slots in one
 // round (less warm-up per sample, no tail round).
 #ifndef MKID_SEG_L
@@ -47,6 +47,23 @@ constexpr int64_t kSegL = MKID_SEG_L;
 constexpr int64_t kSegW = MKID_SEG_W;  // multiple of the 26-sample matched-filter ring
 static_assert(kSegW % kFirTaps == 0 && kSegL >= kSegW + kRawHist, "segment geometry");
 int64_t seg_capacity(int64_t L, int dead) { return L / (dead + 3) + 2; }
+
+// SVF baseline (Chamberlin 2-pole, Kf 82 / Kq 93623 Fix18_16): two integer trajectories started
+// from different states coincide only after ~10^4 samples (the difference decays with the
+// filter's ~1100-sample time constant, then random-walks through the shift roundings to zero:
+// median 1.5e4, 99th percentile 2.9e4, max 3.9e4 over 1024 simulated noisy channels; on the
+// bench stream a 49k-sample warm-up still missed 0.3 % of segments, 98k about 1 in 30000,
+// DESIGN.md §5), so SVF segments speculate from kSvfW samples of warm-up and are at least
+// kSvfLmin long; a segment closer than kSvfW to the sub-chunk start warms up from the carried
+// (exact) state at row 0. Segment lengths are multiples of 26 so that every warm-up start keeps
+// the filter ring aligned. The per-lane walk is latency bound: one segment per two SIMD lanes
+// (svf_lanes) balanced against the warm-up redundancy measured best (tools/svf_sweep.sh).
+#ifndef MKID_SVF_W
+#define MKID_SVF_W (26 * 3780)
+#endif
+constexpr int64_t kSvfW = MKID_SVF_W;
+constexpr int64_t kSvfLmin = 26 * 158;
+static_assert(kSvfW % kFirTaps == 0, "SVF warm-up geometry");
 
 // segment length for J rows: >= kSegL, and (C/64) * ceil(J/L) waves <= the resident slots
 int64_t seg_length(int64_t J, int C, int64_t wave_slots) {
@@ -101,6 +118,7 @@ struct mkid_ctx {
     uint64_t* d_scratch = nullptr;   // [C][capseg]
     int32_t* d_reruns = nullptr;     // [C]
     int64_t nseg_max = 0, slot_cap = 0, scratch_cap = 0, trig_slots = 0;
+    int64_t svf_lanes = 65536, svf_w = kSvfW;  // SVF segmentation (plan_sub)
     int64_t nsub_max = 0;    // sub-chunks per call (ceil(max_chunk / G))
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
     int64_t last_J = 0;     // phase rows of the last call
@@ -343,6 +361,15 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->trig_slots = trigger_wave_slots(device);
     // tuning/test knob: pretend the GPU holds this many trigger waves (forces longer segments)
     if (const char* ev = getenv("MKID_TRIG_WAVE_SLOTS")) c->trig_slots = std::max<int64_t>(1, atoll(ev));
+    {   // SVF segments: one per two SIMD lanes (4 SIMDs x 64 lanes per CU); test/tuning knobs
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        c->svf_lanes = (int64_t)ncu * 128;
+        if (const char* ev = getenv("MKID_SVF_LANES")) c->svf_lanes = std::max<int64_t>(1, atoll(ev));
+        if (const char* ev = getenv("MKID_SVF_WARMUP"))
+            c->svf_w = std::max<int64_t>(1, atoll(ev) / kFirTaps) * kFirTaps;
+    }
     const int64_t Lmax = seg_length(c->Jmax, C, c->trig_slots);
     // for J <= Jmax: L(J) <= Lmax and ceil(J / L(J)) <= max(slots * 64 / C, ceil(Jmax / kSegL))
     c->nseg_max = std::max<int64_t>(std::max<int64_t>(1, c->trig_slots * 64 / C), (c->Jmax + kSegL - 1) / kSegL);
@@ -602,7 +629,27 @@ struct SubPlan {
 };
 
 static SubPlan plan_sub(const mkid_ctx* c, int64_t J) {
-    const bool serial = c->mode == MKID_BASE_SVF || J <= kSegL;
+    if (c->mode == MKID_BASE_SVF) {
+        // svf_lanes segments over all channels (the per-lane walk is latency bound), each
+        // >= kSvfLmin rows; short sub-chunks run as one exact segment
+        const int64_t want = std::max<int64_t>(1, c->svf_lanes / c->C);
+        int64_t nseg = std::min<int64_t>(std::min<int64_t>(want, J / kSvfLmin), c->nseg_max);
+        SubPlan p;
+        p.J = J;
+        p.W = 0;
+        p.L = (int32_t)J;
+        p.nseg = 1;
+        if (nseg > 1 && J > 2 * kSvfLmin) {
+            int64_t L = (J + nseg - 1) / nseg;
+            L = (L + kFirTaps - 1) / kFirTaps * kFirTaps;
+            p.L = (int32_t)L;
+            p.W = (int32_t)c->svf_w;
+            p.nseg = (int32_t)((J + L - 1) / L);
+        }
+        p.capseg = (int32_t)seg_capacity(p.L, c->cfg.dead_time);
+        return p;
+    }
+    const bool serial = J <= kSegL;
     const int64_t Ls = serial ? J : seg_length(J, c->C, c->trig_slots);
     SubPlan p;
     p.J = J;
@@ -615,7 +662,7 @@ static SubPlan plan_sub(const mkid_ctx* c, int64_t J) {
 
 // The sub-chunk plans of a call of n samples and the call's slot-table geometry: stride = total
 // segments per channel, capseg = the largest per-segment capacity (the table is uniform).
-static void plan_call(const mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, int32_t& stride, int32_t& capseg) {
+static int plan_call(mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, int32_t& stride, int32_t& capseg) {
     subs.clear();
     stride = 0;
     capseg = 1;
@@ -623,7 +670,10 @@ static void plan_call(const mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, 
         subs.push_back(plan_sub(c, std::min<int64_t>(c->G, n - off) / c->N));
         stride += subs.back().nseg;
         capseg = std::max(capseg, subs.back().capseg);
+        if (subs.back().nseg > c->nseg_max) FAIL(c, MKID_E_ARG, "trigger plan exceeds the segment tables");
     }
+    if ((int64_t)c->C * stride * capseg > c->slot_cap) FAIL(c, MKID_E_ARG, "trigger plan exceeds the packet slot table");
+    return MKID_OK;
 }
 
 // K7 on stream s for the sub-chunk's phase rows in d_raw: matched filter, baseline, trigger state
@@ -665,7 +715,10 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     hipStream_t s = c->stream;
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
-    plan_call(c, n, subs, stride, capseg);
+    {
+        int r = plan_call(c, n, subs, stride, capseg);
+        if (r) return r;
+    }
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
     HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, s));
     const uint32_t* x = (const uint32_t*)d_iq;
@@ -729,7 +782,10 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     hipStream_t A = c->stream, B = c->sB;
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
-    plan_call(c, n, subs, stride, capseg);
+    {
+        int r = plan_call(c, n, subs, stride, capseg);
+        if (r) return r;
+    }
     // B joins A's order (inputs written by earlier work on A, previous calls) ...
     HIPCHK(c, hipEventRecord(c->ev_start, A));
     HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
@@ -809,7 +865,10 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
     hipStream_t s = c->stream;
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
-    plan_call(c, rows * c->N, subs, stride, capseg);
+    {
+        int r = plan_call(c, rows * c->N, subs, stride, capseg);
+        if (r) return r;
+    }
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
     int32_t seg_off = 0;
     int64_t r0 = 0;

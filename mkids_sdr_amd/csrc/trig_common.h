@@ -135,6 +135,47 @@ __device__ __forceinline__ bool trig_update_fast(FastState& s, int32_t f, const 
     return emit;
 }
 
+// Hot-loop form of trig_update for the SVF mode (same outputs): the code-state machine of
+// trig_update_fast, the Chamberlin update in int64 exactly as trig_update (floor shifts), the
+// baseline settled before the loop. ev.base is low >> 16, the baseline the sample is compared to.
+struct FastSvf {
+    int64_t low, band;
+    int32_t x, f1, f2;
+};
+
+__device__ __forceinline__ FastSvf to_fast_svf(const TrigState& s) {
+    const FastState f = to_fast(s);
+    return FastSvf{s.low, s.band, f.x, f.f1, f.f2};
+}
+
+__device__ __forceinline__ TrigState from_fast_svf(const FastSvf& f) {
+    TrigState t = from_fast(FastState{0, f.x, f.f1, f.f2});
+    t.low = f.low;
+    t.band = f.band;
+    return t;
+}
+
+__device__ __forceinline__ bool trig_update_svf(FastSvf& s, int32_t f, const FastCfg& k, int32_t kf, int32_t kq,
+                                                EvInfo& ev) {
+    const int32_t base = (int32_t)(s.low >> 16);
+    const int32_t e = f - base;
+    ev = EvInfo{s.f2, s.f1, base};
+    if ((uint32_t)e + k.goff < k.glim) {
+        const int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)kq * s.band) >> 16);
+        s.band += ((int64_t)kf * high) >> 16;
+        s.low += ((int64_t)kf * s.band) >> 16;
+    }
+    const int32_t x = s.x;
+    const bool emit = (x == -2) & (f > s.f1);
+    int32_t xn = e < k.thr ? 2 * x : -1;
+    xn = x == -2 ? (f > s.f1 ? k.dx : -2) : xn;
+    xn = x > 0 ? x - 1 : xn;
+    s.x = xn;
+    s.f2 = s.f1;
+    s.f1 = f;
+    return emit;
+}
+
 // Advance state s by one filtered sample f taken at global phase index jg. Returns true and fills
 // *pkt when a packet is emitted (its timestamp is jg - 1: the peak is the previous sample).
 __device__ __forceinline__ bool trig_step(TrigState& s, int32_t f, const TrigCfg& k, int32_t c,

@@ -1,0 +1,79 @@
+"""SVF baseline mode (set_svf.py:10-35, Kf 82 / Kq 93623) on the speculative-segment trigger:
+segments warm up over ~1e5 samples (the two-pole integer baseline needs ~1e4-4e4 samples before
+two trajectories coincide), and every result is bit-exact against the sequential oracle
+(oracle/trigger.c), with and without forced fix-up re-runs."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import trigger as otrig
+from mkids_sdr_amd import codecs
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def synth_raw(C, J, seed, pulse_rate=1.0 / 2000):
+    """Fix16_13 phase rows [J][C]: per-channel offset + white noise (sigma 300) + photon pulses
+    -A (1 - e^{-t/0.1}) e^{-t/65} (pulses.py:470-472), A ~ U(20, 100) deg."""
+    rng = np.random.default_rng(seed)
+    ph = rng.normal(0.0, 300.0, (J, C)) + rng.uniform(-4000, 4000, C)
+    t = np.arange(400, dtype=np.float64)
+    shape = (1 - np.exp(-t / 0.1)) * np.exp(-t / 65.0)
+    for c in range(C):
+        k = rng.poisson(pulse_rate * J)
+        for s0, a in zip(rng.integers(0, J - 400, k), np.deg2rad(rng.uniform(20, 100, k))):
+            ph[s0:s0 + 400, c] -= a * 8192 * shape
+    return np.clip(np.rint(ph), -25736, 25736).astype(np.int16)
+
+
+def run_both(raw, chunks, env=None, monkeypatch=None):
+    from mkids_sdr_amd.channelizer import Channelizer
+    C = raw.shape[1]
+    mf = codecs.fir_quantise(np.loadtxt(os.path.join(GOLD, 'fir', 'matched_30us.txt')))
+    taps = np.tile(mf, (C, 1))
+    quiet = synth_raw(C, 20000, 99, pulse_rate=0)
+    thr = np.array([codecs.threshold_from_phase(quiet[:, c])[0] for c in range(C)], np.int32)
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, str(v))
+    ch = Channelizer(C, max_chunk=max(chunks) * 2 * C)
+    try:
+        ch.set_fir(taps)
+        ch.set_thresholds(thr)
+        ch.set_baseline(2, 41, 82, 93623, 8192)
+        got, reruns, r0 = [], 0, 0
+        for n in chunks:
+            got.append(ch.trigger_phase(raw[r0:r0 + n]))
+            reruns += ch.trigger_reruns()
+            r0 += n
+    finally:
+        ch.close()
+    tr = otrig.Trigger(C, taps, thr, mode=2)
+    exp, r0 = [], 0
+    for n in chunks:
+        exp.append(tr.run(raw[r0:r0 + n])[0])
+        r0 += n
+    return got, exp, reruns
+
+
+@pytest.mark.gpu
+def test_svf_segments_exact(gpu):
+    C, J = 64, 300000
+    raw = synth_raw(C, J, 3)
+    got, exp, reruns = run_both(raw, [J])
+    assert len(exp[0]) > 1000
+    assert np.array_equal(got[0], exp[0])
+    assert reruns <= 3      # warm-up long enough: speculation (almost) never fails on noise
+
+
+@pytest.mark.gpu
+def test_svf_segments_forced_fixup_streamed(gpu, monkeypatch):
+    """A 520-sample warm-up cannot settle the SVF baseline: nearly every segment is re-run by
+    k_trig_fix, the packets must still be exact; streamed in unequal calls (carried state)."""
+    C, J = 64, 160000
+    raw = synth_raw(C, J, 4)
+    got, exp, reruns = run_both(raw, [70000, 90000], env={'MKID_SVF_WARMUP': 520},
+                                monkeypatch=monkeypatch)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    assert reruns > 50

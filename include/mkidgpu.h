@@ -68,7 +68,7 @@ typedef struct mkid_cfg {
     int32_t dds_entries;       /* P = 2^16 / C LO samples per channel; ROACH_Setup.py:521-530 */
     int32_t dead_time;         /* trigger dead time in phase samples (build decision)         */
     int32_t max_events_per_ch; /* per-call event capacity per channel (0 = derive from chunk) */
-    int32_t front;             /* MKID_FRONT_AUTO (fused K1-K6 kernel where N <= 2048) or
+    int32_t front;             /* MKID_FRONT_AUTO (fused K1-K6 kernel, N = 128..4096) or  
                                   MKID_FRONT_SPLIT (channeliser + low-pass kernels, z in HBM)  */
     int64_t max_chunk;         /* largest nsamples per process call (workspace sizing)        */
     double sample_rate;        /* fs, complex S/s; ROACH_Setup.py:82                           */

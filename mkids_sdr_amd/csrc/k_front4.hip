@@ -1,0 +1,362 @@
+// Fused front end for N = 4096 (2048 channels, BASELINE config 5): K1-K6 in one pass over the ADC
+// stream, the complex baseband never leaving the chip (the split path stages it through HBM at
+// +16 B per ADC sample). Same FFT scheme as k_front2.hip (decimation in time by NW = 8 sub-FFTs of
+// 512 points, each computed inside one wave, one cross-wave exchange per frame), re-balanced for
+// a 2048-channel frame:
+//
+//  * a 512-thread workgroup (8 waves, 2 per SIMD, <= 256 VGPRs) walks its run FPB = 2 frames per
+//    iteration; wave w computes sub-FFT w of both frames, thread t then owns the four channels
+//    t + 512 q (q = 0..3) in the select / DDC / low-pass / phase stage;
+//  * the PFB taps of a wave's points are the same every frame, so they live in VGPRs (8 int16
+//    quads per lane) and the LDS holds only the ADC ring (9 hops, 72 KiB), the Y buffers of the two
+//    frames (72 KiB) and the two twiddle tables: 151.5 KiB of the CU's 160 KiB;
+//  * X[bin] = sum_w W_N^{w bin} Y_w[bin mod 512] is evaluated by Horner's rule in W_N^{bin} (one
+//    complex constant per channel instead of seven);
+//  * the decimating low-pass folds its accumulator shift into the output frame's FMAs.
+// Index maps and LDS layouts are those of k_front2.hip at NW = 8 (tools/front2_layouts.py).
+#include "fft_common.h"
+#include "mkid_internal.h"
+
+#ifndef MKID_NT_LOADS
+#define MKID_NT_LOADS 1
+#endif
+#ifndef MKID_NT_STORES
+#define MKID_NT_STORES 1
+#endif
+
+namespace mkid {
+
+namespace {
+
+struct G4 {
+    static constexpr int N = 4096, NW = 8, FPB = 2, BT = 512, CPT = 4;
+    static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
+    static constexpr int RS = 2 * T - 1 + FPB;         // ring slots (hops)
+    static constexpr int Q = M / NW;                   // samples per hop plane
+    static constexpr int REG = 576;                    // float2 per (frame, wave) region
+    static constexpr int FB = NW * REG;                // float2 per frame
+    static constexpr int HIST = (2 * T - 1 + kLpfHist) * M;
+    static constexpr size_t off_fbuf = (size_t)RS * M * 4;
+    static constexpr size_t off_tw1 = off_fbuf + (size_t)FPB * FB * 8;  // W_512^{L k}: [k-1][L]
+    static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;    // W_64^{l k}: [k-1][l]
+    static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
+    static_assert(BT * CPT == C && BT == NW * 64, "geometry");
+    static_assert(BT * 8 == FPB * M, "one 32-byte ring refill per thread per iteration");
+    static_assert(lds_bytes <= 160 * 1024, "LDS");
+};
+
+typedef short fshort2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fshort2_t as_s2(uint32_t v) { return __builtin_bit_cast(fshort2_t, v); }
+__device__ __forceinline__ int32_t dot2_first(uint32_t h, uint32_t x) {
+    int32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(h), "v"(x));
+    return d;
+}
+
+// the 32 bytes (8 samples) this thread contributes to the FPB hops starting at first_hop
+__device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int tid, uint4& v0, uint4& v1) {
+    const int64_t s0 = first_hop * G4::M + (int64_t)tid * 8;
+    if (s0 >= a.K * G4::M) {
+        v0 = v1 = make_uint4(0, 0, 0, 0);
+        return;
+    }
+    if (s0 >= -a.avail) {
+#if MKID_NT_LOADS
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 p = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0));
+        const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0 + 4));
+        v0 = make_uint4(p.x, p.y, p.z, p.w);
+        v1 = make_uint4(q.x, q.y, q.z, q.w);
+#else
+        v0 = *reinterpret_cast<const uint4*>(a.x + s0);
+        v1 = *reinterpret_cast<const uint4*>(a.x + s0 + 4);
+#endif
+        return;
+    }
+    const uint32_t* h = a.xhist + (s0 + a.avail + G4::HIST);
+    v0 = *reinterpret_cast<const uint4*>(h);
+    v1 = *reinterpret_cast<const uint4*>(h + 4);
+}
+
+// samples qoff..qoff+7 of a hop (qoff a multiple of 8) into the permuted hop layout: sample o at
+// (o % 8) Q + o / 8, i.e. one dword in each of the 8 planes (consecutive lanes, consecutive dwords)
+__device__ __forceinline__ void ring_put8(uint32_t* hop, int qoff, uint4 v0, uint4 v1) {
+    constexpr int Q = G4::Q;
+    uint32_t* p = hop + qoff / 8;
+    p[0] = v0.x; p[Q] = v0.y; p[2 * Q] = v0.z; p[3 * Q] = v0.w;
+    p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
+}
+
+template <int BANKS>
+__device__ __forceinline__ float upd_ror8(float old, float src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                 __builtin_bit_cast(int, src), 0x128, 0xf,
+                                                                 BANKS, false));
+}
+
+// register bits <-> lane bits 3-5 (k_front2.hip t1_transpose)
+__device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
+#pragma unroll
+    for (int r0 = 0; r0 < 8; r0 += 2) {
+        const float2 a0 = v[r0], a1 = v[r0 + 1];
+        v[r0].x = upd_ror8<0xC>(a0.x, a1.x);
+        v[r0].y = upd_ror8<0xC>(a0.y, a1.y);
+        v[r0 + 1].x = upd_ror8<0x3>(a1.x, a0.x);
+        v[r0 + 1].y = upd_ror8<0x3>(a1.y, a0.y);
+    }
+    constexpr int kP16[4] = {0, 1, 4, 5};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r0 = kP16[i];
+        const auto sx = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].x),
+                                                         __builtin_bit_cast(int, v[r0 + 2].x), false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].y),
+                                                         __builtin_bit_cast(int, v[r0 + 2].y), false, false);
+        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
+        v[r0 + 2] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
+    }
+#pragma unroll
+    for (int r0 = 0; r0 < 4; ++r0) {
+        const auto sx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].x),
+                                                         __builtin_bit_cast(int, v[r0 + 4].x), false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].y),
+                                                         __builtin_bit_cast(int, v[r0 + 4].y), false, false);
+        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
+        v[r0 + 4] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
+    }
+}
+
+__device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
+
+}  // namespace
+
+__global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
+    using G = G4;
+    constexpr int NW = G::NW, M = G::M, C = G::C, T = G::T, RS = G::RS, FPB = G::FPB, CPT = G::CPT;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
+    float2* fbuf = reinterpret_cast<float2*>(smem + G::off_fbuf);
+    float2* tw1 = reinterpret_cast<float2*>(smem + G::off_tw1);
+    float2* tw2 = reinterpret_cast<float2*>(smem + G::off_tw2);
+
+    const int tid = threadIdx.x;
+    const int L = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave's sub-FFT (both frames)
+
+    for (int i = tid; i < 7 * 64; i += G::BT) {
+        const int k = i / 64 + 1, l = i % 64;
+        double sn, cs;
+        sincospi(-2.0 * (double)(l * k) / 512.0, &sn, &cs);
+        tw1[i] = make_float2((float)cs, (float)sn);
+    }
+    for (int i = tid; i < 7 * 8; i += G::BT) {
+        const int k = i / 8 + 1, l = i % 8;
+        double sn, cs;
+        sincospi(-2.0 * (double)(l * k) / 64.0, &sn, &cs);
+        tw2[i] = make_float2((float)cs, (float)sn);
+    }
+    // PFB tap quads of this lane's points NW (64 r + L) + w, r = 0..7 (fixed for every frame)
+    uint2 tq[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
+
+    // select constants of channels c_q = tid + 512 q
+    float2 tb[CPT];
+    int yoff[CPT];
+    float ic[CPT], qc[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+        const int c = tid + G::BT * q;
+        const int32_t bin = a.bins[c];
+        double sn, cs;
+        sincospi(-2.0 * (double)bin / G::N, &sn, &cs);
+        tb[q] = make_float2((float)cs, (float)sn);
+        yoff[q] = yswz(bin & 511);
+        ic[q] = a.ic[c];
+        qc[q] = a.qc[c];
+    }
+
+    const int64_t k_b = (int64_t)blockIdx.x * a.frames_per_block;
+    int64_t k_e = k_b + a.frames_per_block;
+    if (k_e > a.K) k_e = a.K;
+    if (k_b >= k_e) return;
+    const int64_t k_start = k_b - kLpfHist;
+    int16_t* const raw_run = a.raw + (k_b >> 1) * C;
+    float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
+
+    const int qh = (tid * 8) / M, qoff = (tid * 8) % M;  // this thread's ring write
+    {   // prologue: hops k_start-2T+1 .. k_start+FPB-1 -> ring (slot = hop mod RS)
+        const int64_t h0 = k_start - 2 * T + 1;
+        for (int g = 0; g < RS; g += FPB) {
+            const int64_t hop = h0 + g + qh;
+            if (hop > h0 + RS - 1) continue;
+            uint4 v0, v1;
+            load8(a, h0 + g, tid, v0, v1);
+            ring_put8(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v0, v1);
+        }
+    }
+    uint4 pre0, pre1;
+    load8(a, k_start + FPB, tid, pre0, pre1);
+    __syncthreads();
+
+    float2 acc[CPT][13];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q)
+#pragma unroll
+        for (int m = 0; m < 13; ++m) acc[q][m] = make_float2(0.f, 0.f);
+    float2 ys[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) ys[q] = make_float2(0.f, 0.f);
+
+    int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);
+    int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
+    const int nrun = (int)(k_e - k_b);
+    const int la = L & 7, kl = L >> 3;
+    const float2* t1 = tw1 + L;
+    const float2* t2 = tw2 + la;
+
+    for (int kr = -kLpfHist; kr < nrun; kr += FPB) {
+        float2 lov[FPB][CPT];
+#pragma unroll
+        for (int f = 0; f < FPB; ++f)
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) lov[f][q] = (a.lo + ((lrow + f) & (a.P - 1)) * C)[tid + G::BT * q];
+
+#pragma unroll
+        for (int sl0 = 0; sl0 < FPB; ++sl0) {
+            float2* reg = fbuf + sl0 * G::FB + w * G::REG;
+            // ---- PFB: points NW (64 r + L) + w of frame kb + sl0 ----
+            int sb = rb + sl0;
+            sb -= sb >= RS ? RS : 0;
+            float2 v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int hi = r >> 2;
+                const int pos = w * G::Q + 64 * (r & 3) + L;
+                uint32_t x4[T];
+#pragma unroll
+                for (int tau = 0; tau < T; ++tau) {
+                    int s = sb + 2 * tau + hi;
+                    s -= s >= RS ? RS : 0;
+                    x4[tau] = ring[s * M + pos];
+                }
+                const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
+                const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
+                const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);
+                const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x07060302u);
+                int32_t ai = dot2_first(tq[r].x, i01);
+                ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
+                int32_t aq = dot2_first(tq[r].x, q01);
+                aq = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(q23), aq, false);
+                v[r] = make_float2((float)ai, (float)aq);
+            }
+            // ---- stage 1 + W_512^{L k}, T1, stage 2 + W_64^{la k}, T2 (own region), stage 3 ----
+            dft<8>(v);
+#pragma unroll
+            for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], t1[64 * (k - 1)]);
+            t1_transpose(v);
+            dft<8>(v);
+#pragma unroll
+            for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], t2[8 * (k - 1)]);
+            float2* t2w = reg + 72 * kl + la;
+            const float2* t2r = reg + 72 * kl + 9 * la;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) t2w[9 * r] = v[r];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = t2r[r];
+            dft<8>(v);
+            __builtin_amdgcn_wave_barrier();
+            float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
+#pragma unroll
+            for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
+        }
+        __syncthreads();  // Y of both frames visible; every ring read of this iteration done
+
+        {   // ring refill for the next iteration (its oldest FPB hops), prefetch one further
+            int ws = rb + qh;
+            ws -= ws >= RS ? RS : 0;
+            ring_put8(ring + ws * M, qoff, pre0, pre1);
+            load8(a, k_b + kr + 2 * FPB, tid, pre0, pre1);
+            rb += FPB;
+            rb -= rb >= RS ? RS : 0;
+            lrow += FPB;
+        }
+
+        // ---- select (Horner in W_N^bin) + DDC + low-pass + phase, channels tid + 512 q ----
+#pragma unroll
+        for (int f = 0; f < FPB; ++f) {
+            const int kf = kr + f;
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                const float2* yf = fbuf + f * G::FB + yoff[q];
+                float2 X = yf[7 * G::REG];
+#pragma unroll
+                for (int s = 6; s >= 0; --s) X = cmac(yf[s * G::REG], X, tb[q]);
+                const float2 z = cmul(X, lov[f][q]);
+                if ((f & 1) == 0) {
+#pragma unroll
+                    for (int m = 0; m < 13; ++m) {
+                        acc[q][m].x = fmaf(a.taps.g[2 * m + 1], z.x, acc[q][m].x);
+                        acc[q][m].y = fmaf(a.taps.g[2 * m + 1], z.y, acc[q][m].y);
+                    }
+                } else {
+                    // output frame: accumulate and shift to the next output in one FMA each
+                    const float2 y = make_float2(fmaf(a.taps.g[0], z.x, acc[q][0].x),
+                                                 fmaf(a.taps.g[0], z.y, acc[q][0].y));
+#pragma unroll
+                    for (int m = 0; m < 12; ++m) {
+                        acc[q][m].x = fmaf(a.taps.g[2 * m + 2], z.x, acc[q][m + 1].x);
+                        acc[q][m].y = fmaf(a.taps.g[2 * m + 2], z.y, acc[q][m + 1].y);
+                    }
+                    acc[q][12] = make_float2(0.f, 0.f);
+                    if (kf > 0 && kf < nrun) {
+                        const int c = tid + G::BT * q;
+                        const int jr = (kf - 1) >> 1;
+                        ys[q].x += y.x;
+                        ys[q].y += y.y;
+                        const float ph = phase_atan2(y.y - qc[q], y.x - ic[q]);
+                        int qv = __float2int_rn(ph * 8192.0f);
+                        qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
+#if MKID_NT_STORES
+                        if (phase_run) __builtin_nontemporal_store(ph, phase_run + jr * C + c);
+                        __builtin_nontemporal_store((int16_t)qv, raw_run + jr * C + c);
+#else
+                        if (phase_run) (phase_run + jr * C)[c] = ph;
+                        (raw_run + jr * C)[c] = (int16_t)qv;
+#endif
+                        if (c == a.iq_ch && a.iqtap) {
+                            a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y.x);
+                            a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y.y);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();  // select reads done before the next iteration's region writes
+    }
+    if (a.ysum)
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) ysum_add(a.ysum, tid + G::BT * q, ys[q].x, ys[q].y);
+}
+
+bool front4_supported(int N) { return N == G4::N; }
+
+hipError_t launch_front4(const FrontArgs& a0, hipStream_t s) {
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front4, (int)G4::lds_bytes);
+    if (e != hipSuccess) return e;
+    FrontArgs a = a0;
+    if (a.K <= 0) return hipSuccess;
+    // runs of 256..1024 frames (the 24-frame low-pass warm-up is 2.3-9 % of a run), >= 1024 runs
+    // for a full chunk so that the 256 CUs see four waves of workgroups
+    int64_t fpb = a.K / 1024;
+    fpb = fpb < 64 ? 64 : (fpb > 1024 ? 1024 : fpb);
+    fpb = (fpb + G4::FPB - 1) / G4::FPB * G4::FPB;
+    a.frames_per_block = fpb;
+    const int64_t blocks = (a.K + fpb - 1) / fpb;
+    hipLaunchKernelGGL(k_front4, dim3((unsigned)blocks), dim3(G4::BT), G4::lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mkid

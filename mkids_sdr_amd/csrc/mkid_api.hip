@@ -104,7 +104,7 @@ struct mkid_ctx {
     hipEvent_t ev_start = nullptr, ev_done = nullptr;
     int zi = 0;
     int64_t G = 0;  // pipeline sub-chunk (samples)
-    bool fused = false;  // K1-K6 in k_front (no z buffers, no stream B work)
+    bool fused = false;  // K1-K6 in one kernel (k_front / k_front2 / k_front4: no z buffers, no stream B work)
     bool front_v2 = false;  // fused front end is k_front2 (N = 512..2048; MKID_FRONT_V1=1 forces v1)
     int64_t H = 0;       // ADC history samples carried between calls
     // workspace
@@ -338,7 +338,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->cfg = *cfg;
     c->device = device;
     c->C = C; c->N = N; c->M = N / 2; c->T = kPfbTaps; c->P = P;
-    c->fused = cfg->front == MKID_FRONT_AUTO && front_supported(N);
+    c->fused = cfg->front == MKID_FRONT_AUTO && (front_supported(N) || front4_supported(N));
     {
         const char* v1 = getenv("MKID_FRONT_V1");
         c->front_v2 = c->fused && front2_supported(N) && !(v1 && atoi(v1) != 0);
@@ -748,7 +748,8 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
         tstart(c, MKID_K_FRONT, &kt, s);
-        HIPCHK(c, c->front_v2 ? launch_front2(N, fa, s) : launch_front(N, fa, s));
+        HIPCHK(c, front4_supported(N) ? launch_front4(fa, s)
+                                      : (c->front_v2 ? launch_front2(N, fa, s) : launch_front(N, fa, s)));
         tstop(c, &kt, s);
         int r = run_trigger(c, c->d_raw, subs[si], stride, seg_off, capseg, s);
         if (r) return r;

@@ -178,6 +178,8 @@ bool channelize_supported(int N);
 bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length
 bool front2_supported(int N);        // the one-exchange fused kernel (k_front2.hip) for this N
 hipError_t launch_front2(int N, const FrontArgs& a, hipStream_t s);
+bool front4_supported(int N);        // the 2048-channel fused kernel (k_front4.hip, N = 4096)
+hipError_t launch_front4(const FrontArgs& a, hipStream_t s);
 int64_t front_hist_samples(int N);  // ADC history the fused kernel reads before a chunk
 
 }  // namespace mkid

@@ -117,11 +117,13 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     (512, 2 ** 18, None, 4, 'auto'),
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'auto'),    # config 3 geometry
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'split'),
-    (2048, 2 ** 20, None, 6, 'auto'),               # config 5 geometry (split front: N = 4096)
+    (2048, 2 ** 20, [0, 3 * 2 ** 17 + 4096, 2 ** 20], 6, 'auto'),   # config 5 geometry (k_front4)
+    (2048, 2 ** 20, None, 6, 'split'),
 ])
 def test_chain_parity(gpu, C, S, splits, seed, front):
-    """Full chain vs the oracle. 'auto' runs the fused k_front kernel for N <= 2048; 'split'
-    runs k_channelize + k_lpf_phase with z staged in HBM."""
+    """Full chain vs the oracle. 'auto' runs the fused front end (k_front2 for N = 512..2048,
+    k_front4 for N = 4096, k_front for N = 128); 'split' runs k_channelize + k_lpf_phase with z
+    staged in HBM."""
     case = signals.make_case(C, S, seed=seed, pulses_per_ch=max(1.0, S / (2 * C) / 400))
     thr = quiet_thresholds(C, min(S, 2 * C * 2048), seed)
     compare(case, thr, splits or [0, S], front=front)

@@ -52,6 +52,22 @@ def decimation_combine(N, seed=1):
     return np.abs(X - np.fft.fft(u)).max()
 
 
+def horner_combine_f32(N=4096, seed=2):
+    """k_front4.hip's select: X[b] = Y_0 + t (Y_1 + t (... + t Y_7)), t = W_N^b, in complex64
+    (as the device's fp32 cmac chain); returns the max error relative to max |X|."""
+    rng = np.random.default_rng(seed)
+    u = (rng.normal(size=N) + 1j * rng.normal(size=N)) * 3e4
+    NW = N // 512
+    Ys = [np.fft.fft(u[w::NW]).astype(np.complex64) for w in range(NW)]
+    k = np.arange(N)
+    t = np.exp(-2j * np.pi * k / N).astype(np.complex64)
+    X = Ys[NW - 1][k % 512]
+    for w in range(NW - 2, -1, -1):
+        X = (Ys[w][k % 512] + X * t).astype(np.complex64)
+    ref = np.fft.fft(u)
+    return float(np.abs(X - ref).max() / np.abs(ref).max())
+
+
 def _groups(width):
     """lane groups (one LDS cycle each) and bank count of an instruction (MI355X_MICROARCH.md)."""
     if width == 'r32':
@@ -90,8 +106,13 @@ def check_layouts(N):
                           for w in range(NW) for r in range(8))
     ok['tap_read'] = all(conflict_free(lambda L, w=w, r=r: 2 * (w * 512 + 64 * r + L), 2, 'r64')
                          for w in range(NW) for r in range(8))
-    # ring writes: thread t writes samples 4t'..4t'+3 (t' = t mod M/4) of one hop
-    if NW == 4:
+    # ring writes: thread t writes samples 4t'..4t'+3 (t' = t mod M/4) of one hop (8t'..8t'+7
+    # at NW = 8: one dword in each plane)
+    if NW == 8:
+        ok['ring_write'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')
+                               for j in range(8) for b in range(0, M // 8, 64))
+        ok['tap_read'] = True   # k_front4 holds the taps in VGPRs
+    elif NW == 4:
         ok['ring_write'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')
                                for j in range(4) for b in range(0, M // 4, 64))
     elif NW == 2:
@@ -114,5 +135,6 @@ def check_layouts(N):
 
 if __name__ == '__main__':
     print('fft emulation max error', fft_emulation())
-    for N in (512, 1024, 2048):
+    for N in (512, 1024, 2048, 4096):
         print(N, 'combine error', decimation_combine(N), check_layouts(N))
+    print('4096 Horner combine (fp32) relative error', horner_combine_f32())

@@ -287,47 +287,66 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
 #pragma unroll
         for (int f = 0; f < FPB; ++f) {
             const int kf = kr + f;
+            const float2* yf = fbuf + f * G::FB;
+            float2 z[CPT];
 #pragma unroll
             for (int q = 0; q < CPT; ++q) {
-                const float2* yf = fbuf + f * G::FB + yoff[q];
-                float2 X = yf[7 * G::REG];
+                // all eight reads of the channel issued before its Horner chain
+                float2 yv[NW];
 #pragma unroll
-                for (int s = 6; s >= 0; --s) X = cmac(yf[s * G::REG], X, tb[q]);
-                const float2 z = cmul(X, lov[f][q]);
-                if ((f & 1) == 0) {
+                for (int sg = 0; sg < NW; ++sg) yv[sg] = yf[yoff[q] + sg * G::REG];
+                float2 X = yv[NW - 1];
 #pragma unroll
-                    for (int m = 0; m < 13; ++m) {
-                        acc[q][m].x = fmaf(a.taps.g[2 * m + 1], z.x, acc[q][m].x);
-                        acc[q][m].y = fmaf(a.taps.g[2 * m + 1], z.y, acc[q][m].y);
+                for (int sg = NW - 2; sg >= 0; --sg) X = cmac(yv[sg], X, tb[q]);
+                z[q] = cmul(X, lov[f][q]);
+            }
+            if ((f & 1) == 0) {
+#pragma unroll
+                for (int m = 0; m < 13; ++m)
+#pragma unroll
+                    for (int q = 0; q < CPT; ++q) {
+                        acc[q][m].x = fmaf(a.taps.g[2 * m + 1], z[q].x, acc[q][m].x);
+                        acc[q][m].y = fmaf(a.taps.g[2 * m + 1], z[q].y, acc[q][m].y);
                     }
-                } else {
-                    // output frame: accumulate and shift to the next output in one FMA each
-                    const float2 y = make_float2(fmaf(a.taps.g[0], z.x, acc[q][0].x),
-                                                 fmaf(a.taps.g[0], z.y, acc[q][0].y));
+            } else {
+                // output frame: accumulate and shift to the next output in one FMA each
+                float2 y[CPT];
 #pragma unroll
-                    for (int m = 0; m < 12; ++m) {
-                        acc[q][m].x = fmaf(a.taps.g[2 * m + 2], z.x, acc[q][m + 1].x);
-                        acc[q][m].y = fmaf(a.taps.g[2 * m + 2], z.y, acc[q][m + 1].y);
+                for (int q = 0; q < CPT; ++q)
+                    y[q] = make_float2(fmaf(a.taps.g[0], z[q].x, acc[q][0].x), fmaf(a.taps.g[0], z[q].y, acc[q][0].y));
+#pragma unroll
+                for (int m = 0; m < 12; ++m)
+#pragma unroll
+                    for (int q = 0; q < CPT; ++q) {
+                        acc[q][m].x = fmaf(a.taps.g[2 * m + 2], z[q].x, acc[q][m + 1].x);
+                        acc[q][m].y = fmaf(a.taps.g[2 * m + 2], z[q].y, acc[q][m + 1].y);
                     }
-                    acc[q][12] = make_float2(0.f, 0.f);
-                    if (kf > 0 && kf < nrun) {
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) acc[q][12] = make_float2(0.f, 0.f);
+                if (kf > 0 && kf < nrun) {
+                    const int jr = (kf - 1) >> 1;
+                    float ph[CPT];
+#pragma unroll
+                    for (int q = 0; q < CPT; ++q) {
+                        ys[q].x += y[q].x;
+                        ys[q].y += y[q].y;
+                        ph[q] = phase_atan2(y[q].y - qc[q], y[q].x - ic[q]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < CPT; ++q) {
                         const int c = tid + G::BT * q;
-                        const int jr = (kf - 1) >> 1;
-                        ys[q].x += y.x;
-                        ys[q].y += y.y;
-                        const float ph = phase_atan2(y.y - qc[q], y.x - ic[q]);
-                        int qv = __float2int_rn(ph * 8192.0f);
+                        int qv = __float2int_rn(ph[q] * 8192.0f);
                         qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
 #if MKID_NT_STORES
-                        if (phase_run) __builtin_nontemporal_store(ph, phase_run + jr * C + c);
+                        if (phase_run) __builtin_nontemporal_store(ph[q], phase_run + jr * C + c);
                         __builtin_nontemporal_store((int16_t)qv, raw_run + jr * C + c);
 #else
-                        if (phase_run) (phase_run + jr * C)[c] = ph;
+                        if (phase_run) (phase_run + jr * C)[c] = ph[q];
                         (raw_run + jr * C)[c] = (int16_t)qv;
 #endif
                         if (c == a.iq_ch && a.iqtap) {
-                            a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y.x);
-                            a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y.y);
+                            a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y[q].x);
+                            a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y[q].y);
                         }
                     }
                 }
@@ -348,9 +367,13 @@ hipError_t launch_front4(const FrontArgs& a0, hipStream_t s) {
     if (e != hipSuccess) return e;
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
-    // runs of 256..1024 frames (the 24-frame low-pass warm-up is 2.3-9 % of a run), >= 1024 runs
-    // for a full chunk so that the 256 CUs see four waves of workgroups
-    int64_t fpb = a.K / 1024;
+    // runs of up to 1024 frames (the 24-frame low-pass warm-up is 2.3 % of a full run): a full
+    // 2^30-sample chunk is MKID_F4_BLOCKS workgroups, two rounds over the 256 CUs (-2.2 % against
+    // 1024 runs of 512 frames, tools/kbench.py A/B)
+#ifndef MKID_F4_BLOCKS
+#define MKID_F4_BLOCKS 512
+#endif
+    int64_t fpb = a.K / MKID_F4_BLOCKS;
     fpb = fpb < 64 ? 64 : (fpb > 1024 ? 1024 : fpb);
     fpb = (fpb + G4::FPB - 1) / G4::FPB * G4::FPB;
     a.frames_per_block = fpb;

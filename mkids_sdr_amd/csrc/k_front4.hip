@@ -218,9 +218,14 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
     for (int kr = -kLpfHist; kr < nrun; kr += FPB) {
         float2 lov[FPB][CPT];
 #pragma unroll
-        for (int f = 0; f < FPB; ++f)
+        for (int f = 0; f < FPB; ++f) {
+            // scalar row base + 32-bit lane offsets: global_load with an SGPR base, no 64-bit
+            // per-lane address arithmetic
+            const char* row = reinterpret_cast<const char*>(a.lo + ((lrow + f) & (a.P - 1)) * C);
 #pragma unroll
-            for (int q = 0; q < CPT; ++q) lov[f][q] = (a.lo + ((lrow + f) & (a.P - 1)) * C)[tid + G::BT * q];
+            for (int q = 0; q < CPT; ++q)
+                lov[f][q] = *reinterpret_cast<const float2*>(row + (uint32_t)(tid + G::BT * q) * 8u);
+        }
 
 #pragma unroll
         for (int sl0 = 0; sl0 < FPB; ++sl0) {

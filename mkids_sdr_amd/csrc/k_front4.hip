@@ -10,8 +10,8 @@
 //  * the PFB taps of a wave's points are the same every frame, so they live in VGPRs (8 int16
 //    quads per lane) and the LDS holds only the ADC ring (9 hops, 72 KiB), the Y buffers of the two
 //    frames (72 KiB) and the two twiddle tables: 151.5 KiB of the CU's 160 KiB;
-//  * X[bin] = sum_w W_N^{w bin} Y_w[bin mod 512] is evaluated by Horner's rule in W_N^{bin} (one
-//    complex constant per channel instead of seven);
+//  * X[bin] = sum_w W_N^{w bin} Y_w[bin mod 512] is evaluated as two 4-term Horner chains in
+//    W_N^{bin} joined by W_N^{4 bin} (two complex constants per channel instead of seven);
 //  * the decimating low-pass folds its accumulator shift into the output frame's FMAs.
 // Index maps and LDS layouts are those of k_front2.hip at NW = 8 (tools/front2_layouts.py).
 #include "fft_common.h"
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
     for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
 
     // select constants of channels c_q = tid + 512 q
-    float2 tb[CPT];
+    float2 tb[CPT], tb4[CPT];   // W_N^{bin}, W_N^{4 bin}
     int yoff[CPT];
     float ic[CPT], qc[CPT];
 #pragma unroll
@@ -171,6 +171,8 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
         double sn, cs;
         sincospi(-2.0 * (double)bin / G::N, &sn, &cs);
         tb[q] = make_float2((float)cs, (float)sn);
+        sincospi(-2.0 * (double)((4 * bin) % G::N) / G::N, &sn, &cs);
+        tb4[q] = make_float2((float)cs, (float)sn);
         yoff[q] = yswz(bin & 511);
         ic[q] = a.ic[c];
         qc[q] = a.qc[c];
@@ -300,10 +302,15 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
                 float2 yv[NW];
 #pragma unroll
                 for (int sg = 0; sg < NW; ++sg) yv[sg] = yf[yoff[q] + sg * G::REG];
-                float2 X = yv[NW - 1];
+                // two 4-term Horner chains joined by the exact W_N^{4 bin}: half the rounding
+                // depth of one 8-term chain (the phase bar is 1e-5 rad), and two chains of ILP
+                float2 Xl = yv[3], Xh = yv[7];
 #pragma unroll
-                for (int sg = NW - 2; sg >= 0; --sg) X = cmac(yv[sg], X, tb[q]);
-                z[q] = cmul(X, lov[f][q]);
+                for (int sg = 2; sg >= 0; --sg) {
+                    Xl = cmac(yv[sg], Xl, tb[q]);
+                    Xh = cmac(yv[sg + 4], Xh, tb[q]);
+                }
+                z[q] = cmul(cmac(Xl, Xh, tb4[q]), lov[f][q]);
             }
             if ((f & 1) == 0) {
 #pragma unroll

@@ -104,6 +104,12 @@ struct mkid_ctx {
     hipEvent_t ev_start = nullptr, ev_done = nullptr;
     int zi = 0;
     int64_t G = 0;  // pipeline sub-chunk (samples)
+    int64_t pipe_G = 0;  // fused front end: sub-chunk of the two-stream pipeline (0 = off)
+    // matched filter as the lean trigger needs it: one tap row shared by every live channel
+    bool taps_uniform = true;
+    int16_t utaps[kFirTaps] = {0};
+    uint8_t* d_live = nullptr;      // [C] 1: the shared taps, 0: all-zero taps
+    int64_t last_raw_row = 0;       // first row of the last sub-chunk's raw phase in d_raw
     bool fused = false;  // K1-K6 in one kernel (k_front / k_front2 / k_front4: no z buffers, no stream B work)
     bool front_v2 = false;  // fused front end is k_front2 (N = 512..2048; MKID_FRONT_V1=1 forces v1)
     int64_t H = 0;       // ADC history samples carried between calls
@@ -210,7 +216,8 @@ static void free_all(mkid_ctx* c) {
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
-                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff};
+                    c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff,
+                    c->d_live};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -354,6 +361,22 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->Kmax = G / c->M;
     c->Jmax = G / N;
     c->nsub_max = (cfg->max_chunk + G - 1) / G;
+    // fused front end, two-stream pipeline (opt-in, MKID_PIPE_MIN_CHUNK): a call of >= pipe_min
+    // samples runs as 4 sub-chunks, the front end of sub-chunk i+1 (stream A) beside the trigger of
+    // sub-chunk i (stream B, the lean variant: resident next to the front end's waves). d_raw
+    // holds the whole call, one region per sub-chunk. Off by default: measured same-box at config
+    // 3 it does not pay (5.49 ms/step without, 5.99-6.13 with, profiles/r02_v7_kbench_pipeline.json):
+    // the front end leaves too few issue cycles for the resident trigger to hide in.
+#ifndef MKID_PIPE_MIN
+#define MKID_PIPE_MIN ((int64_t)1 << 62)
+#endif
+    int64_t pipe_min = MKID_PIPE_MIN;
+    if (const char* ev = getenv("MKID_PIPE_MIN_CHUNK")) pipe_min = std::max<int64_t>(4 * N, atoll(ev));  // tests
+    if (c->fused && cfg->max_chunk >= pipe_min) {
+        c->pipe_G = cfg->max_chunk / 4;
+        c->pipe_G -= c->pipe_G % N;
+        c->nsub_max = std::max<int64_t>(c->nsub_max, (cfg->max_chunk + c->pipe_G - 1) / c->pipe_G);
+    }
     // Packet capacities are hard bounds: an event needs >= dead_time + 3 phase samples (trigger,
     // peak, dead time, re-arm), so no per-channel/segment overflow can occur.
     const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // whole call, one segment
@@ -425,6 +448,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_scratch, (size_t)C * c->scratch_cap);
     AL(d_reruns, C);
     AL(d_counts, 2);
+    AL(d_live, C);
 #undef AL
     // defaults: identity bins, unit LO, Blackman 250 kHz low-pass, zero matched filter (no
     // triggers), zero centres, thresholds off, EMA baseline alpha=41 gate=8192.
@@ -435,13 +459,15 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     std::vector<float2> lo((size_t)C * P, make_float2(32767.f / 32768.f, 0.f));
     std::vector<int16_t> fir((size_t)C * kFirTaps, 0);
     std::vector<float> zero(C, 0.f);
+    std::vector<uint8_t> dead(C, 0);   // default matched filter: all-zero taps (uniform, none live)
     for (int i = 0; i < kFirTaps; ++i) c->lpf.g[i] = kBlackman250k[i] / 2048.0f;
     if ((e = hipMemcpy(c->d_bins, bins.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_thr, thr.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_lo, lo.data(), lo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_fir, fir.data(), fir.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_ic, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_qc, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        (e = hipMemcpy(c->d_qc, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_live, dead.data(), C, hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "hipMemcpy defaults");
     c->h_lo = lo;
     c->h_bins = bins;
@@ -572,7 +598,27 @@ int mkid_set_fir(mkid_ctx* c, const int16_t* taps, int32_t nch, int32_t nt) {
     if (nch != c->C || nt != kFirTaps) FAIL(c, MKID_E_ARG, "matched filter must be [C][26]");
     for (int64_t i = 0; i < (int64_t)nch * nt; ++i)
         if (taps[i] < -2048 || taps[i] > 2047) FAIL(c, MKID_E_ARG, "matched-filter tap outside 12-bit range");
-    return upload(c, c->d_fir, taps, (size_t)nch * nt * 2);
+    // uniform: every channel's row is either the first non-zero row or all zero (the reference
+    // loads one LUT file for every channel and zeroes deleted ones, ROACH_Pulses.py:59-111)
+    const int16_t* shared = nullptr;
+    std::vector<uint8_t> live((size_t)nch, 0);
+    bool uniform = true;
+    for (int ch = 0; ch < nch && uniform; ++ch) {
+        const int16_t* row = taps + (size_t)ch * nt;
+        bool zero = true;
+        for (int i = 0; i < nt; ++i) zero = zero && row[i] == 0;
+        if (zero) continue;
+        if (!shared) shared = row;
+        uniform = std::equal(row, row + nt, shared);
+        live[ch] = 1;
+    }
+    int r = upload(c, c->d_fir, taps, (size_t)nch * nt * 2);
+    if (r) return r;
+    r = upload(c, c->d_live, live.data(), (size_t)nch);
+    if (r) return r;
+    c->taps_uniform = uniform;
+    for (int i = 0; i < kFirTaps; ++i) c->utaps[i] = shared ? shared[i] : 0;
+    return MKID_OK;
 }
 
 int mkid_set_centers(mkid_ctx* c, const float* ic, const float* qc, int32_t n) {
@@ -618,6 +664,7 @@ int mkid_reset_stream(mkid_ctx* c) {
     c->j0 = 0;
     c->last_J = 0;
     c->last_subJ = 0;
+    c->last_raw_row = 0;
     return MKID_OK;
 }
 
@@ -650,7 +697,8 @@ static SubPlan plan_sub(const mkid_ctx* c, int64_t J) {
         return p;
     }
     const bool serial = J <= kSegL;
-    const int64_t Ls = serial ? J : seg_length(J, c->C, c->trig_slots);
+    // segment starts at multiples of 26 (the lean trigger's window is group-aligned)
+    const int64_t Ls = serial ? J : (seg_length(J, c->C, c->trig_slots) + kFirTaps - 1) / kFirTaps * kFirTaps;
     SubPlan p;
     p.J = J;
     p.L = (int32_t)Ls;
@@ -662,12 +710,13 @@ static SubPlan plan_sub(const mkid_ctx* c, int64_t J) {
 
 // The sub-chunk plans of a call of n samples and the call's slot-table geometry: stride = total
 // segments per channel, capseg = the largest per-segment capacity (the table is uniform).
-static int plan_call(mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, int32_t& stride, int32_t& capseg) {
+static int plan_call(mkid_ctx* c, int64_t n, int64_t G, std::vector<SubPlan>& subs, int32_t& stride,
+                     int32_t& capseg) {
     subs.clear();
     stride = 0;
     capseg = 1;
-    for (int64_t off = 0; off < n; off += c->G) {
-        subs.push_back(plan_sub(c, std::min<int64_t>(c->G, n - off) / c->N));
+    for (int64_t off = 0; off < n; off += G) {
+        subs.push_back(plan_sub(c, std::min<int64_t>(G, n - off) / c->N));
         stride += subs.back().nseg;
         capseg = std::max(capseg, subs.back().capseg);
         if (subs.back().nseg > c->nseg_max) FAIL(c, MKID_E_ARG, "trigger plan exceeds the segment tables");
@@ -680,7 +729,7 @@ static int plan_call(mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, int32_t
 // machine (speculative segments + fix-up) into segments seg_off.. of the call's slot table, then
 // the raw-phase history roll. Compaction (K8) runs once per call (compact_call).
 static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32_t stride, int32_t seg_off,
-                       int32_t capseg, hipStream_t s) {
+                       int32_t capseg, hipStream_t s, bool lean = false) {
     const int C = c->C;
     KTime kt;
     TrigSpecArgs ta{raw,        c->d_rhist, c->d_fir,   c->d_thr,      c->d_tstate,  c->d_tstate,
@@ -688,6 +737,14 @@ static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32
                     sp.J,       c->j0,      C,          sp.nseg,       sp.L,         sp.W,
                     capseg,     c->mode,    c->alpha,   c->kf,         c->kq,        c->base_thr,
                     c->cfg.dead_time, stride, seg_off};
+    if (lean) {
+        auto p2 = [](int16_t lo, int16_t hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); };
+        ta.live = c->d_live;
+        for (int m = 0; m < kFirTaps / 2; ++m) ta.utap[m] = p2(c->utaps[2 * m], c->utaps[2 * m + 1]);
+        for (int m = 0; m < kFirTaps / 2 - 1; ++m) ta.utapb[m] = p2(c->utaps[2 * m + 1], c->utaps[2 * m + 2]);
+        ta.utap0 = p2(c->utaps[0], 0);
+        ta.utap25 = p2(c->utaps[kFirTaps - 1], 0);
+    }
     tstart(c, MKID_K_TRIGGER, &kt, s);
     HIPCHK(c, launch_trigger(ta, s));
     tstop(c, &kt, s);
@@ -707,27 +764,43 @@ static int compact_call(mkid_ctx* c, int32_t stride, int32_t capseg, uint64_t* d
     return MKID_OK;
 }
 
-// Fused front end: one k_front launch per sub-chunk (ADC -> phase, raw), then K7, all on the
-// context stream; one compaction per call.
+// Fused front end: one front-end launch per sub-chunk (ADC -> phase, raw), then K7, one
+// compaction per call. A long call (pipe_G) with a lean-eligible trigger (uniform matched-filter
+// taps, EMA / no baseline) runs as a two-stream pipeline: the front end of sub-chunk i+1 on
+// stream A while the lean trigger of sub-chunk i runs on stream B, resident beside it; every
+// sub-chunk writes its own region of d_raw, so A never waits for B inside a call. Otherwise all
+// on the context stream.
 static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
                          int64_t cap, int64_t* d_counts) {
     const int C = c->C, N = c->N, M = c->M;
-    hipStream_t s = c->stream;
+    // k_front4 (2 waves/SIMD, latency bound) is slowed more by a resident trigger wave than the
+    // trigger's time is worth (config 5: 8.6 -> 11.6 ms/step measured), so only k_front2 pipelines
+    const bool pipe = c->pipe_G > 0 && n > c->pipe_G && c->taps_uniform && c->front_v2 &&
+                      (c->mode == MKID_BASE_EMA || c->mode == MKID_BASE_NONE);
+    // the lean trigger has no start-of-stream hold-off path: every state is past it once more
+    // than kHoldOff rows have been processed since the reset
+    const int64_t G = pipe ? c->pipe_G : c->G;
+    hipStream_t A = c->stream, B = pipe ? c->sB : c->stream;
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
     {
-        int r = plan_call(c, n, subs, stride, capseg);
+        int r = plan_call(c, n, G, subs, stride, capseg);
         if (r) return r;
     }
-    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, s));
+    if (pipe) {   // B joins A's order (inputs written by earlier work on A, previous calls)
+        HIPCHK(c, hipEventRecord(c->ev_start, A));
+        HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
+    }
+    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, B));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, A));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
     int32_t seg_off = 0;
     size_t si = 0;
-    for (int64_t off = 0; off < n; off += c->G, ++si) {
-        const int64_t S = std::min<int64_t>(c->G, n - off);
+    for (int64_t off = 0; off < n; off += G, ++si) {
+        const int64_t S = std::min<int64_t>(G, n - off);
         const int64_t K = S / M, J = S / N;
+        int16_t* raw = c->d_raw + (off / N) * C;
         KTime kt;
         FrontArgs fa{};
         fa.x = x + off;
@@ -738,7 +811,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.ic = c->d_ic;
         fa.qc = c->d_qc;
         fa.phase = d_phase ? d_phase + (off / N) * C : nullptr;
-        fa.raw = c->d_raw;
+        fa.raw = raw;
         fa.ysum = c->d_ysum;
         fa.K = K;
         fa.k0 = c->k0;
@@ -747,24 +820,35 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.taps = c->lpf;
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
-        tstart(c, MKID_K_FRONT, &kt, s);
-        HIPCHK(c, front4_supported(N) ? launch_front4(fa, s)
-                                      : (c->front_v2 ? launch_front2(N, fa, s) : launch_front(N, fa, s)));
-        tstop(c, &kt, s);
-        int r = run_trigger(c, c->d_raw, subs[si], stride, seg_off, capseg, s);
+        tstart(c, MKID_K_FRONT, &kt, A);
+        HIPCHK(c, front4_supported(N) ? launch_front4(fa, A)
+                                      : (c->front_v2 ? launch_front2(N, fa, A) : launch_front(N, fa, A)));
+        tstop(c, &kt, A);
+        if (pipe) {
+            HIPCHK(c, hipEventRecord(c->ev_zready[si & 1], A));
+            HIPCHK(c, hipStreamWaitEvent(B, c->ev_zready[si & 1], 0));
+        }
+        // the last sub-chunk's trigger runs alone: the regular kernel, which fills the GPU
+        const bool last = off + S >= n;
+        int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, B, pipe && !last && c->j0 > kHoldOff);
         if (r) return r;
         seg_off += subs[si].nseg;
         c->k0 += K;
         c->j0 += J;
         c->last_J += J;
         c->last_subJ = J;
+        c->last_raw_row = off / N;
     }
     {
-        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, s);
+        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, B);
         if (r) return r;
     }
-    HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, c->H, n, 4, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)c->H * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, c->H, n, 4, A));
+    HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)c->H * 4, hipMemcpyDeviceToDevice, A));
+    if (pipe) {   // ... and A (the caller's stream) waits for everything B did
+        HIPCHK(c, hipEventRecord(c->ev_done, B));
+        HIPCHK(c, hipStreamWaitEvent(A, c->ev_done, 0));
+    }
     c->iq_rows = c->iq_ch >= 0 ? n / N : 0;
     return MKID_OK;
 }
@@ -784,7 +868,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
     {
-        int r = plan_call(c, n, subs, stride, capseg);
+        int r = plan_call(c, n, c->G, subs, stride, capseg);
         if (r) return r;
     }
     // B joins A's order (inputs written by earlier work on A, previous calls) ...
@@ -842,6 +926,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
         c->j0 += J;
         c->last_J += J;
         c->last_subJ = J;
+        c->last_raw_row = 0;
     }
     {
         int r = compact_call(c, stride, capseg, d_events, cap, d_counts, B);
@@ -867,7 +952,7 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
     {
-        int r = plan_call(c, rows * c->N, subs, stride, capseg);
+        int r = plan_call(c, rows * c->N, c->G, subs, stride, capseg);
         if (r) return r;
     }
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
@@ -926,7 +1011,7 @@ int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, ui
 
 int mkid_last_raw_phase(mkid_ctx* c, const int16_t** d_raw, int64_t* nrows) {
     if (!c || !d_raw || !nrows) return MKID_E_ARG;
-    *d_raw = c->d_raw;
+    *d_raw = c->d_raw + c->last_raw_row * c->C;
     *nrows = std::min(c->last_subJ, c->Jmax);
     return MKID_OK;
 }
@@ -938,7 +1023,8 @@ int mkid_read_raw_phase(mkid_ctx* c, int16_t* host_out, int64_t cap_rows, int64_
     const int64_t n = std::min(avail, cap_rows);
     if (n <= 0) return MKID_OK;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpyAsync(host_out, c->d_raw, (size_t)n * c->C * 2, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(host_out, c->d_raw + c->last_raw_row * c->C, (size_t)n * c->C * 2,
+                             hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return MKID_OK;
 }

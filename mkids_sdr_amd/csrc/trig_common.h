@@ -121,8 +121,10 @@ __device__ __forceinline__ bool trig_update_fast(FastState& s, int32_t f, const 
     const int32_t e = f - s.B;
     ev = EvInfo{s.f2, s.f1, s.B};
     if (MODE == MKID_BASE_EMA) {
-        const bool gate = (uint32_t)e + k.goff < k.glim;
-        s.B += gate ? (__mul24(k.alpha, e) >> 9) : 0;
+        // branch-free: as a branch the update splits every sample into its own block, and the
+        // register allocator of the unrolled 26-sample groups spills across them
+        const int32_t gate = -(int32_t)((uint32_t)e + k.goff < k.glim);
+        s.B += (__mul24(k.alpha, e) >> 9) & gate;
     }
     const int32_t x = s.x;
     const bool emit = (x == -2) & (f > s.f1);

@@ -266,3 +266,28 @@ def test_iq_snapshot_tap_matches_oracle(gpu, front):
         assert ch.iq_tap().shape == (0, 2)
     finally:
         ch.close()
+
+
+@pytest.mark.parametrize('C,S,splits,seed,mode,deleted', [
+    (64, 2 ** 16, None, 31, 1, False),
+    (256, 2 ** 18, [0, 2 ** 17 + 512, 2 ** 18], 32, 1, True),
+    (256, 2 ** 18, None, 33, 0, False),
+    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 34, 1, False),      # k_front2, N = 2048
+    (2048, 2 ** 20, [0, 2 ** 19 + 4096, 2 ** 20], 35, 1, True),  # k_front4, N = 4096
+])
+def test_fused_two_stream_pipeline(gpu, monkeypatch, C, S, splits, seed, mode, deleted):
+    """process_fused's pipeline (front end of sub-chunk i+1 on stream A beside the lean trigger of
+    sub-chunk i on stream B; forced here at small sizes with MKID_PIPE_MIN_CHUNK) against the
+    oracle: uniform matched-filter taps (zero rows = deleted channels), EMA and no-baseline modes,
+    streamed calls (the first sub-chunk after the reset runs the regular trigger, the rest the
+    lean one)."""
+    monkeypatch.setenv('MKID_PIPE_MIN_CHUNK', str(8 * 2 * C))
+    case = signals.make_case(C, S, seed=seed, pulses_per_ch=max(2.0, S / (2 * C) / 400))
+    if deleted:
+        case.fir12[1::3] = 0
+    thr = quiet_thresholds(C, min(S, 2 * C * 2048), seed)
+    if mode == 0:
+        o = signals.oracle_chain(case)
+        raw = o.process(case.iq)['raw'].astype(np.int64)
+        thr = (np.median(raw, axis=0) * 1.38 - 1500).astype(np.int64)
+    compare(case, thr, splits or [0, S], mode=mode)

@@ -53,17 +53,21 @@ def decimation_combine(N, seed=1):
 
 
 def horner_combine_f32(N=4096, seed=2):
-    """k_front4.hip's select: X[b] = Y_0 + t (Y_1 + t (... + t Y_7)), t = W_N^b, in complex64
-    (as the device's fp32 cmac chain); returns the max error relative to max |X|."""
+    """k_front4.hip's select: X[b] = (Y_0 + t (Y_1 + t (Y_2 + t Y_3))) + t4 (Y_4 + t (... + t Y_7)),
+    t = W_N^b and t4 = W_N^{4b} (both rounded from float64), in complex64 as the device's fp32 cmac
+    chains; returns the max error relative to max |X|."""
     rng = np.random.default_rng(seed)
     u = (rng.normal(size=N) + 1j * rng.normal(size=N)) * 3e4
     NW = N // 512
     Ys = [np.fft.fft(u[w::NW]).astype(np.complex64) for w in range(NW)]
     k = np.arange(N)
     t = np.exp(-2j * np.pi * k / N).astype(np.complex64)
-    X = Ys[NW - 1][k % 512]
-    for w in range(NW - 2, -1, -1):
-        X = (Ys[w][k % 512] + X * t).astype(np.complex64)
+    t4 = np.exp(-2j * np.pi * ((4 * k) % N) / N).astype(np.complex64)
+    lo, hi = Ys[3][k % 512], Ys[7][k % 512]
+    for w in (2, 1, 0):
+        lo = (Ys[w][k % 512] + lo * t).astype(np.complex64)
+        hi = (Ys[w + 4][k % 512] + hi * t).astype(np.complex64)
+    X = (lo + hi * t4).astype(np.complex64)
     ref = np.fft.fft(u)
     return float(np.abs(X - ref).max() / np.abs(ref).max())
 

@@ -157,15 +157,28 @@ __device__ __forceinline__ TrigState from_fast_svf(const FastSvf& f) {
     return t;
 }
 
+// a * b (mod 2^64, i.e. the int64 product whenever it does not overflow) for 0 <= a < 2^32:
+// v_mad_u64_u32 + v_mul_lo_u32, where the generic int64 x int64 product takes three multiplies
+__device__ __forceinline__ int64_t mul_u32_i64(uint32_t a, int64_t b) {
+    const uint64_t lo = (uint64_t)a * (uint32_t)b;
+    const uint32_t hi = a * (uint32_t)((uint64_t)b >> 32);
+    return (int64_t)(lo + ((uint64_t)hi << 32));
+}
+
 __device__ __forceinline__ bool trig_update_svf(FastSvf& s, int32_t f, const FastCfg& k, int32_t kf, int32_t kq,
                                                 EvInfo& ev) {
     const int32_t base = (int32_t)(s.low >> 16);
     const int32_t e = f - base;
     ev = EvInfo{s.f2, s.f1, base};
-    if ((uint32_t)e + k.goff < k.glim) {
-        const int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)kq * s.band) >> 16);
-        s.band += ((int64_t)kf * high) >> 16;
-        s.low += ((int64_t)kf * s.band) >> 16;
+    {   // computed unconditionally and selected (a branch per sample splits the unrolled groups
+        // into blocks the register allocator spills across)
+        const bool gate = (uint32_t)e + k.goff < k.glim;
+        // kf, kq are Fix18_16 in 0..2^18-1 (mkid_set_baseline checks)
+        const int64_t high = ((int64_t)f << 16) - s.low - (mul_u32_i64((uint32_t)kq, s.band) >> 16);
+        const int64_t band = s.band + (mul_u32_i64((uint32_t)kf, high) >> 16);
+        const int64_t low = s.low + (mul_u32_i64((uint32_t)kf, band) >> 16);
+        s.band = gate ? band : s.band;
+        s.low = gate ? low : s.low;
     }
     const int32_t x = s.x;
     const bool emit = (x == -2) & (f > s.f1);

@@ -50,6 +50,16 @@ __device__ __forceinline__ float2 cmac(float2 x, float2 t, float2 y) {
     return float2_of(d);
 }
 
+// y * t as one v_pk_mul_f32 + one v_pk_fma_f32 (the plain cmul above compiles to four scalar
+// FP32 ops where the operands come straight from LDS)
+__device__ __forceinline__ float2 cmul_pk(float2 y, float2 t) {
+    f2v d;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]\n\t"
+        "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+        : "=&v"(d) : "v"(f2v_of(y)), "v"(f2v_of(t)));
+    return float2_of(d);
+}
+
 __device__ __forceinline__ void dft2(float2& a, float2& b) {
     float2 t = a;
     a = cadd(t, b);

@@ -54,6 +54,10 @@
 #define MKID_NT_STORES 1
 #endif
 
+#ifndef MKID_CMUL
+#define MKID_CMUL cmul_pk
+#endif
+
 namespace mkid {
 
 namespace {
@@ -304,12 +308,12 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
         // ---- stage 1 + twiddle W_512^{L k} ----
         dft<8>(v);
 #pragma unroll
-        for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], t1[64 * (k - 1)]);
+        for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t1[64 * (k - 1)]);
         // ---- T1 (VALU cross-lane) + stage 2 + twiddle W_64^{la k} ----
         t1_transpose(v);
         dft<8>(v);
 #pragma unroll
-        for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], t2[8 * (k - 1)]);
+        for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t2[8 * (k - 1)]);
         // ---- T2 through the wave's own region (no workgroup barrier) ----
 #pragma unroll
         for (int r = 0; r < 8; ++r) t2w[9 * r] = v[r];
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
             float2 X = yf[0];
 #pragma unroll
             for (int q = 1; q < NW; ++q) X = cmac(X, tl[q - 1], yf[q * G::REG]);
-            const float2 z = cmul(X, lov[f]);
+            const float2 z = MKID_CMUL(X, lov[f]);
             if ((f & 1) == 0) {
 #pragma unroll
                 for (int m = 0; m < 13; ++m) {

@@ -260,11 +260,11 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
             // ---- stage 1 + W_512^{L k}, T1, stage 2 + W_64^{la k}, T2 (own region), stage 3 ----
             dft<8>(v);
 #pragma unroll
-            for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], t1[64 * (k - 1)]);
+            for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], t1[64 * (k - 1)]);
             t1_transpose(v);
             dft<8>(v);
 #pragma unroll
-            for (int k = 1; k < 8; ++k) v[k] = cmul(v[k], t2[8 * (k - 1)]);
+            for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], t2[8 * (k - 1)]);
             float2* t2w = reg + 72 * kl + la;
             const float2* t2r = reg + 72 * kl + 9 * la;
 #pragma unroll
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
                     Xl = cmac(yv[sg], Xl, tb[q]);
                     Xh = cmac(yv[sg + 4], Xh, tb[q]);
                 }
-                z[q] = cmul(cmac(Xl, Xh, tb4[q]), lov[f][q]);
+                z[q] = cmul_pk(cmac(Xl, Xh, tb4[q]), lov[f][q]);
             }
             if ((f & 1) == 0) {
 #pragma unroll

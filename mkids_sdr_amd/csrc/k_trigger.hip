@@ -25,6 +25,10 @@
 namespace mkid {
 
 constexpr int kSpecThreads = 256;
+// full trigger steps at the end of a speculative warm-up (groups of 26 samples): the state machine
+// forgets a guessed start within the dead time plus one threshold crossing; earlier warm-up
+// samples advance only the baseline (the SVF warm-up is ~10^5 samples, the EMA one 520)
+constexpr int32_t kFullWarm = 100;
 
 __device__ __attribute__((noinline)) uint64_t make_packet(int32_t c, EvInfo ev, int32_t f, int64_t jg) {
     return pack_wide(c, peakfit_i(ev.y1, ev.y2, f), ev.base, jg - 1);
@@ -131,6 +135,10 @@ struct Stepper {
     TrigCfg k;
     __device__ Stepper(const TrigState& s, const TrigCfg& kk, int32_t) : st(s), k(kk) {}
     __device__ __forceinline__ bool step(int32_t f, EvInfo& ev) { return trig_update(st, f, k, ev); }
+    __device__ __forceinline__ void step_base(int32_t f) {
+        EvInfo ev;
+        (void)trig_update(st, f, k, ev);
+    }
     __device__ __forceinline__ TrigState state() const { return st; }
 };
 
@@ -144,6 +152,7 @@ struct Stepper<MODE, true> {
         if (!s.binit) fs.B = MODE == MKID_BASE_NONE ? 0 : f0;
     }
     __device__ __forceinline__ bool step(int32_t f, EvInfo& ev) { return trig_update_fast<MODE>(fs, f, q, ev); }
+    __device__ __forceinline__ void step_base(int32_t f) { base_update_fast<MODE>(fs, f, q); }
     __device__ __forceinline__ TrigState state() const { return from_fast(fs); }
 };
 
@@ -160,6 +169,7 @@ struct Stepper<MKID_BASE_SVF, true> {
         }
     }
     __device__ __forceinline__ bool step(int32_t f, EvInfo& ev) { return trig_update_svf(fs, f, q, kf, kq, ev); }
+    __device__ __forceinline__ void step_base(int32_t f) { base_update_svf(fs, f, q, kf, kq); }
     __device__ __forceinline__ TrigState state() const { return from_fast_svf(fs); }
 };
 
@@ -196,8 +206,16 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
     const int32_t f0 = mf_q(w0, tp, 0, rload(roff));
     const TrigState st0 = jw == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
     auto body = [&](auto& sp) {
-        // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0
-        run_groups(__builtin_amdgcn_readfirstlane((int32_t)(seg0 - jw) / kFirTaps), rbase, roff, (uint32_t)(2 * C),
+        // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0. A long
+        // speculative warm-up (SVF) advances only the baseline until its last kFullWarm groups
+        const int32_t wg = __builtin_amdgcn_readfirstlane((int32_t)(seg0 - jw) / kFirTaps);
+        int32_t wbase = 0;
+        if constexpr (MODE == MKID_BASE_SVF && std::is_same<std::decay_t<decltype(sp)>, Stepper<MODE, true>>::value) {
+            wbase = (jw > 0 && wg > kFullWarm) ? wg - kFullWarm : 0;
+            run_groups(wbase, rbase, roff, (uint32_t)(2 * C),
+                       [&](int32_t, int u, uint32_t r) { sp.step_base(mf_q(win, tp, u, r)); });
+        }
+        run_groups(wg - wbase, rbase, roff, (uint32_t)(2 * C),
                    [&](int32_t, int u, uint32_t r) {
                        EvInfo ev;
                        (void)sp.step(mf_q(win, tp, u, r), ev);

@@ -165,6 +165,18 @@ __device__ __forceinline__ int64_t mul_u32_i64(uint32_t a, int64_t b) {
     return (int64_t)(lo + ((uint64_t)hi << 32));
 }
 
+__device__ __forceinline__ void base_update_svf(FastSvf& s, int32_t f, const FastCfg& k, int32_t kf, int32_t kq) {
+    const int32_t e = f - (int32_t)(s.low >> 16);
+    const bool gate = (uint32_t)e + k.goff < k.glim;
+    const int64_t high = ((int64_t)f << 16) - s.low - (mul_u32_i64((uint32_t)kq, s.band) >> 16);
+    const int64_t band = s.band + (mul_u32_i64((uint32_t)kf, high) >> 16);
+    const int64_t low = s.low + (mul_u32_i64((uint32_t)kf, band) >> 16);
+    s.band = gate ? band : s.band;
+    s.low = gate ? low : s.low;
+    s.f2 = s.f1;
+    s.f1 = f;
+}
+
 __device__ __forceinline__ bool trig_update_svf(FastSvf& s, int32_t f, const FastCfg& k, int32_t kf, int32_t kq,
                                                 EvInfo& ev) {
     const int32_t base = (int32_t)(s.low >> 16);
@@ -189,6 +201,21 @@ __device__ __forceinline__ bool trig_update_svf(FastSvf& s, int32_t f, const Fas
     s.f2 = s.f1;
     s.f1 = f;
     return emit;
+}
+
+// Baseline-only forms for the early part of a long speculative warm-up: the baseline (EMA B /
+// SVF low, band) and the last two samples advance, the trigger state machine does not. Whatever
+// state machine code results is re-converged by the full steps of the warm-up's last part and,
+// like every speculated start state, verified exactly by k_trig_fix.
+template <int MODE>
+__device__ __forceinline__ void base_update_fast(FastState& s, int32_t f, const FastCfg& k) {
+    if (MODE == MKID_BASE_EMA) {
+        const int32_t e = f - s.B;
+        const int32_t gate = -(int32_t)((uint32_t)e + k.goff < k.glim);
+        s.B += (__mul24(k.alpha, e) >> 9) & gate;
+    }
+    s.f2 = s.f1;
+    s.f1 = f;
 }
 
 // Advance state s by one filtered sample f taken at global phase index jg. Returns true and fills

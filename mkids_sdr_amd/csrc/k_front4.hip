@@ -4,9 +4,11 @@
 // 512 points, each computed inside one wave, one cross-wave exchange per frame), re-balanced for
 // a 2048-channel frame:
 //
-//  * a 512-thread workgroup (8 waves, 2 per SIMD, <= 256 VGPRs) walks its run FPB = 2 frames per
-//    iteration; wave w computes sub-FFT w of both frames, thread t then owns the four channels
-//    t + 512 q (q = 0..3) in the select / DDC / low-pass / phase stage;
+//  * a 1024-thread workgroup (16 waves, 4 per SIMD, <= 128 VGPRs) walks its run FPB = 2 frames per
+//    iteration; wave (s, w) computes sub-FFT w of frame s, thread t then owns the two channels
+//    t + 1024 q (q = 0, 1) in the select / DDC / low-pass / phase stage. (MKID_F4_BT=512: 8 waves,
+//    2 per SIMD, 4 channels per thread, no spills, 7 % slower: two waves per SIMD cannot hide the
+//    barrier phases; the 1024-thread build spills ~21 loop-invariant dwords and still wins);
 //  * the PFB taps of a wave's points are the same every frame, so they live in VGPRs (8 int16
 //    quads per lane) and the LDS holds only the ADC ring (9 hops, 72 KiB), the Y buffers of the two
 //    frames (72 KiB) and the two twiddle tables: 151.5 KiB of the CU's 160 KiB;
@@ -28,8 +30,13 @@ namespace mkid {
 
 namespace {
 
+#ifndef MKID_F4_BT
+#define MKID_F4_BT 1024
+#endif
 struct G4 {
-    static constexpr int N = 4096, NW = 8, FPB = 2, BT = 512, CPT = 4;
+    static constexpr int N = 4096, NW = 8, FPB = 2, BT = MKID_F4_BT, CPT = 2048 / BT;
+    static constexpr int SPW = FPB * NW * 64 / BT;     // sub-FFTs per wave per iteration
+    static constexpr int SPT = FPB * (N / 2) / BT;     // ring-refill samples per thread (8 or 4)
     static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
     static constexpr int RS = 2 * T - 1 + FPB;         // ring slots (hops)
     static constexpr int Q = M / NW;                   // samples per hop plane
@@ -40,8 +47,7 @@ struct G4 {
     static constexpr size_t off_tw1 = off_fbuf + (size_t)FPB * FB * 8;  // W_512^{L k}: [k-1][L]
     static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;    // W_64^{l k}: [k-1][l]
     static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
-    static_assert(BT * CPT == C && BT == NW * 64, "geometry");
-    static_assert(BT * 8 == FPB * M, "one 32-byte ring refill per thread per iteration");
+    static_assert(BT * CPT == C && SPW * BT == FPB * NW * 64 && (SPT == 8 || SPT == 4), "geometry");
     static_assert(lds_bytes <= 160 * 1024, "LDS");
 };
 
@@ -53,9 +59,10 @@ __device__ __forceinline__ int32_t dot2_first(uint32_t h, uint32_t x) {
     return d;
 }
 
-// the 32 bytes (8 samples) this thread contributes to the FPB hops starting at first_hop
+// the SPT samples (SPT*4 bytes) this thread contributes to the FPB hops starting at first_hop
 __device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int tid, uint4& v0, uint4& v1) {
-    const int64_t s0 = first_hop * G4::M + (int64_t)tid * 8;
+    constexpr int SPT = G4::SPT;
+    const int64_t s0 = first_hop * G4::M + (int64_t)tid * SPT;
     if (s0 >= a.K * G4::M) {
         v0 = v1 = make_uint4(0, 0, 0, 0);
         return;
@@ -64,27 +71,32 @@ __device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int
 #if MKID_NT_LOADS
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 p = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0));
-        const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0 + 4));
         v0 = make_uint4(p.x, p.y, p.z, p.w);
-        v1 = make_uint4(q.x, q.y, q.z, q.w);
+        if constexpr (SPT == 8) {
+            const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0 + 4));
+            v1 = make_uint4(q.x, q.y, q.z, q.w);
+        }
 #else
         v0 = *reinterpret_cast<const uint4*>(a.x + s0);
-        v1 = *reinterpret_cast<const uint4*>(a.x + s0 + 4);
+        if constexpr (SPT == 8) v1 = *reinterpret_cast<const uint4*>(a.x + s0 + 4);
 #endif
         return;
     }
     const uint32_t* h = a.xhist + (s0 + a.avail + G4::HIST);
     v0 = *reinterpret_cast<const uint4*>(h);
-    v1 = *reinterpret_cast<const uint4*>(h + 4);
+    if constexpr (SPT == 8) v1 = *reinterpret_cast<const uint4*>(h + 4);
 }
 
 // samples qoff..qoff+7 of a hop (qoff a multiple of 8) into the permuted hop layout: sample o at
 // (o % 8) Q + o / 8, i.e. one dword in each of the 8 planes (consecutive lanes, consecutive dwords)
+// (SPT = 4: samples qoff..qoff+3 go to planes qoff % 8 .. + 3; lanes 2k, 2k+1 share a bank, 2-way)
 __device__ __forceinline__ void ring_put8(uint32_t* hop, int qoff, uint4 v0, uint4 v1) {
     constexpr int Q = G4::Q;
-    uint32_t* p = hop + qoff / 8;
+    uint32_t* p = hop + (qoff % 8) * Q + qoff / 8;
     p[0] = v0.x; p[Q] = v0.y; p[2 * Q] = v0.z; p[3 * Q] = v0.w;
-    p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
+    if constexpr (G4::SPT == 8) {
+        p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
+    }
 }
 
 template <int BANKS>
@@ -130,7 +142,7 @@ __device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
 
 }  // namespace
 
-__global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
+__global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
     using G = G4;
     constexpr int NW = G::NW, M = G::M, C = G::C, T = G::T, RS = G::RS, FPB = G::FPB, CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -141,7 +153,10 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
 
     const int tid = threadIdx.x;
     const int L = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave's sub-FFT (both frames)
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = wave % NW;                   // this wave's sub-FFT
+    const int slot0 = (wave / NW) * G::SPW;    // its first frame slot (SPW consecutive slots)
+
 
     for (int i = tid; i < 7 * 64; i += G::BT) {
         const int k = i / 64 + 1, l = i % 64;
@@ -186,7 +201,7 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
     int16_t* const raw_run = a.raw + (k_b >> 1) * C;
     float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
 
-    const int qh = (tid * 8) / M, qoff = (tid * 8) % M;  // this thread's ring write
+    const int qh = (tid * G::SPT) / M, qoff = (tid * G::SPT) % M;  // this thread's ring write
     {   // prologue: hops k_start-2T+1 .. k_start+FPB-1 -> ring (slot = hop mod RS)
         const int64_t h0 = k_start - 2 * T + 1;
         for (int g = 0; g < RS; g += FPB) {
@@ -197,7 +212,7 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
             ring_put8(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v0, v1);
         }
     }
-    uint4 pre0, pre1;
+    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0;
     load8(a, k_start + FPB, tid, pre0, pre1);
     __syncthreads();
 
@@ -218,19 +233,24 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
     const float2* t2 = tw2 + la;
 
     for (int kr = -kLpfHist; kr < nrun; kr += FPB) {
+        // LO rows of the iteration's frames: scalar row base + 32-bit lane offsets (global_load
+        // with an SGPR base). Loaded here (live across the FFT) with 512-thread workgroups; with
+        // 1024 (2 channels per thread, 128 VGPRs) after the FFT, where the registers are free
         float2 lov[FPB][CPT];
+        auto load_lo = [&]() {
 #pragma unroll
-        for (int f = 0; f < FPB; ++f) {
-            // scalar row base + 32-bit lane offsets: global_load with an SGPR base, no 64-bit
-            // per-lane address arithmetic
-            const char* row = reinterpret_cast<const char*>(a.lo + ((lrow + f) & (a.P - 1)) * C);
+            for (int f = 0; f < FPB; ++f) {
+                const char* row = reinterpret_cast<const char*>(a.lo + ((lrow + f) & (a.P - 1)) * C);
 #pragma unroll
-            for (int q = 0; q < CPT; ++q)
-                lov[f][q] = *reinterpret_cast<const float2*>(row + (uint32_t)(tid + G::BT * q) * 8u);
-        }
+                for (int q = 0; q < CPT; ++q)
+                    lov[f][q] = *reinterpret_cast<const float2*>(row + (uint32_t)(tid + G::BT * q) * 8u);
+            }
+        };
+        if constexpr (G::BT == 512) load_lo();
 
 #pragma unroll
-        for (int sl0 = 0; sl0 < FPB; ++sl0) {
+        for (int si = 0; si < G::SPW; ++si) {
+            const int sl0 = slot0 + si;
             float2* reg = fbuf + sl0 * G::FB + w * G::REG;
             // ---- PFB: points NW (64 r + L) + w of frame kb + sl0 ----
             int sb = rb + sl0;
@@ -279,6 +299,7 @@ __global__ __launch_bounds__(G4::BT, 2) void k_front4(FrontArgs a) {
             for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
         }
         __syncthreads();  // Y of both frames visible; every ring read of this iteration done
+        if constexpr (G::BT != 512) load_lo();
 
         {   // ring refill for the next iteration (its oldest FPB hops), prefetch one further
             int ws = rb + qh;

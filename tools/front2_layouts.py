@@ -87,6 +87,20 @@ def _groups(width):
     raise ValueError(width)
 
 
+def conflict_degree(dword_addr_of_lane, ndw, width):
+    """max distinct dwords any bank serves within one lane group (1 = conflict-free)."""
+    groups, nb = _groups(width)
+    deg = 1
+    for g in groups:
+        banks = {}
+        for L in g:
+            a = dword_addr_of_lane(L)
+            for d in range(ndw):
+                banks.setdefault((a + d) % nb, set()).add(a + d)
+        deg = max(deg, max(len(v) for v in banks.values()))
+    return deg
+
+
 def conflict_free(dword_addr_of_lane, ndw, width):
     groups, nb = _groups(width)
     for g in groups:
@@ -113,8 +127,13 @@ def check_layouts(N):
     # ring writes: thread t writes samples 4t'..4t'+3 (t' = t mod M/4) of one hop (8t'..8t'+7
     # at NW = 8: one dword in each plane)
     if NW == 8:
-        ok['ring_write'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')
-                               for j in range(8) for b in range(0, M // 8, 64))
+        # k_front4 (1024 threads): 4 samples per thread, lane t at plane 4 (t & 1) + i, index
+        # t >> 1 -> lanes 2k, 2k+1 share a bank: 2-way on the 4 refill writes per iteration (the
+        # 512-thread build's 8-sample writes are conflict-free)
+        ok['ring_write'] = max(conflict_degree(lambda L, i=i, b=b: (4 * ((b + L) & 1) + i) * Q + ((b + L) >> 1), 1, 'w32')
+                               for i in range(4) for b in range(0, M // 4, 64)) <= 2
+        ok['ring_write8'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')
+                                for j in range(8) for b in range(0, M // 8, 64))
         ok['tap_read'] = True   # k_front4 holds the taps in VGPRs
     elif NW == 4:
         ok['ring_write'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')

@@ -235,9 +235,11 @@ int mkid_optimal_filter(mkid_ctx* ctx, const double* d_template, const double* d
  * mkid_set_pulse_filter: host coeff [nch = C][ncoeff] fp32, 1 <= ncoeff <= 4096, 0 <= pre.
  * mkid_pulse_heights: d_phase holds the device phase rows of global phase indices
  * j0 .. j0 + rows - 1 ([rows][C], e.g. the d_phase of one mkid_process_device call; j0 = the
- * number of phase rows processed before it since the last reset); d_events n wide packets;
- * d_heights n floats, NaN where the window is not inside the rows. Asynchronous on the context
- * stream; device pointers only. */
+ * number of phase rows processed before it since the last reset); d_events n wide packets
+ * (28-bit stamps unwrapped into [j0 - 2^27, j0 + 2^27)); d_heights n floats. The context keeps
+ * the last ncoeff rows it was given: when a call's j0 continues the previous call's rows, windows
+ * that start before row j0 read them. NaN where the window is not inside (carried rows, rows).
+ * Asynchronous on the context stream; device pointers only. */
 int mkid_set_pulse_filter(mkid_ctx* ctx, const float* coeff, int32_t nch, int32_t ncoeff, int32_t pre);
 int mkid_pulse_heights(mkid_ctx* ctx, const float* d_phase, int64_t rows, int64_t j0,
                        const uint64_t* d_events, int64_t n, float* d_heights);

@@ -7,8 +7,9 @@
 // One wave per packet: lane l accumulates taps l, l + 64, ... in fp32, then a fixed-order xor
 // butterfly over the wave (deterministic). The phase rows of one packet's window are strided by
 // C floats, so each lane's read is its own cache line; the volume is small (ncoeff x 4 B per
-// packet, ~3 MB per 2^30 ADC samples at the bench's packet rate) and L2-resident right after the
-// front end wrote it.
+// packet). Windows that start before the call's first row read the context's carried history of
+// the previous call's last rows (mkid_api.hip pulse_heights), so a streamed run loses heights
+// only at the stream start and for windows past the call's last row.
 #include "mkid_internal.h"
 
 namespace mkid {
@@ -25,15 +26,20 @@ __global__ __launch_bounds__(64 * kHeightWaves) void k_pulse_heights(HeightArgs 
         const uint64_t w = a.events[p];
         const int ch = (int)((w >> MKID_PKT_CH_SHIFT) & 0xFFF);
         const int64_t ts = (int64_t)(w & MKID_PKT_TS_MASK);
-        // global phase index of the packet: the 28-bit stamp unwrapped against the rows' origin j0
-        const int64_t jg = a.j0 + ((ts - (a.j0 & (int64_t)MKID_PKT_TS_MASK)) & (int64_t)MKID_PKT_TS_MASK);
-        const int64_t r0 = jg - a.j0 - a.pre;  // first phase row of the window
-        const bool inside = ch < a.C && r0 >= 0 && r0 + a.ncoeff <= a.rows;
+        // global phase index of the packet: the 28-bit stamp unwrapped into [j0 - 2^27, j0 + 2^27)
+        // (a packet emitted at a call's first sample is stamped at the previous call's last row)
+        const int64_t base = a.j0 > ((int64_t)1 << 27) ? a.j0 - ((int64_t)1 << 27) : 0;
+        const int64_t jg = base + ((ts - (base & (int64_t)MKID_PKT_TS_MASK)) & (int64_t)MKID_PKT_TS_MASK);
+        const int64_t r0 = jg - a.j0 - a.pre;  // first phase row of the window (< 0: history)
+        const bool inside = ch < a.C && r0 >= -a.hrows && r0 + a.ncoeff <= a.rows;
         float acc = 0.f;
         if (inside) {
             const float* cf = a.coeff + (size_t)ch * a.ncoeff;
-            const float* ph = a.phase + r0 * a.C + ch;
-            for (int i = lane; i < a.ncoeff; i += 64) acc = fmaf(cf[i], ph[(int64_t)i * a.C], acc);
+            for (int i = lane; i < a.ncoeff; i += 64) {
+                const int64_t r = r0 + i;
+                const float v = r >= 0 ? a.phase[r * a.C + ch] : a.hist[(a.hrows + r) * a.C + ch];
+                acc = fmaf(cf[i], v, acc);
+            }
         }
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);

@@ -134,6 +134,8 @@ struct mkid_ctx {
     int16_t* d_iqtap = nullptr;     // [max_chunk/N][2]
     float* d_hcoeff = nullptr;      // [C][h_ncoeff] pulse-height filter (mkid_set_pulse_filter)
     int32_t h_ncoeff = 0, h_pre = 0;
+    float *d_phist = nullptr, *d_phist_tmp = nullptr;  // [h_ncoeff][C] last phase rows seen by pulse_heights
+    int64_t phist_end = -1, phist_rows = 0;          // global row after its last row; valid rows
     int64_t iq_rows = 0;
     // host copies behind the folded LO table (d_lo = conj(LUT)/2^15 with the (-1)^(b (k+1))
     // bin-parity sign of K4 folded in: P is even, so the sign depends on k mod P only)
@@ -217,7 +219,7 @@ static void free_all(mkid_ctx* c) {
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
                     c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff,
-                    c->d_live};
+                    c->d_live,  c->d_phist, c->d_phist_tmp};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -665,6 +667,8 @@ int mkid_reset_stream(mkid_ctx* c) {
     c->last_J = 0;
     c->last_subJ = 0;
     c->last_raw_row = 0;
+    c->phist_end = -1;     // pulse-height phase history: a reset starts a new stream
+    c->phist_rows = 0;
     return MKID_OK;
 }
 
@@ -1180,6 +1184,15 @@ int mkid_set_pulse_filter(mkid_ctx* c, const float* coeff, int32_t nch, int32_t 
         c->d_hcoeff = nullptr;
     }
     HIPCHK(c, dalloc(&c->d_hcoeff, (size_t)nch * ncoeff));
+    if (c->d_phist) {
+        HIPCHK(c, hipFree(c->d_phist));
+        HIPCHK(c, hipFree(c->d_phist_tmp));
+        c->d_phist = c->d_phist_tmp = nullptr;
+    }
+    HIPCHK(c, dalloc(&c->d_phist, (size_t)nch * ncoeff));
+    HIPCHK(c, dalloc(&c->d_phist_tmp, (size_t)nch * ncoeff));
+    c->phist_end = -1;
+    c->phist_rows = 0;
     c->h_ncoeff = ncoeff;
     c->h_pre = pre;
     return upload(c, c->d_hcoeff, coeff, (size_t)nch * ncoeff * 4);
@@ -1191,11 +1204,23 @@ static int pulse_heights(mkid_ctx* c, const float* d_phase, int64_t rows, int64_
     if (rows < 0 || j0 < 0 || n < 0) FAIL(c, MKID_E_ARG, "pulse heights: negative rows/j0/n");
     if (!c->d_hcoeff) FAIL(c, MKID_E_STATE, "pulse heights: no filter set (mkid_set_pulse_filter)");
     HIPCHK(c, hipSetDevice(c->device));
-    HeightArgs a{d_phase, d_events, c->d_hcoeff, d_heights, rows, j0, n, c->C, c->h_ncoeff, c->h_pre, d_n};
+    // the carried rows precede this call's rows only if the calls are contiguous in j
+    const int64_t hrows = (c->phist_end == j0) ? c->phist_rows : 0;
+    const int64_t H = c->h_ncoeff;   // d_phist: H rows, the valid ones are its last phist_rows
+    HeightArgs a{d_phase, d_events, c->d_hcoeff, d_heights, rows, j0, n, c->C, c->h_ncoeff, c->h_pre, d_n,
+                 c->d_phist + (H - hrows) * c->C, hrows};
     KTime kt;
     tstart(c, MKID_K_HEIGHTS, &kt, c->stream);
     HIPCHK(c, launch_pulse_heights(a, c->stream));
     tstop(c, &kt, c->stream);
+    // keep the last H rows of (history, these rows) for the next call's early windows
+    if (rows > 0) {
+        HIPCHK(c, launch_hist_roll(c->d_phist_tmp, c->d_phist, d_phase, H, rows, (int64_t)c->C * 4, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_phist, c->d_phist_tmp, (size_t)H * c->C * 4, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        c->phist_rows = std::min<int64_t>(H, hrows + rows);
+        c->phist_end = j0 + rows;
+    }
     return MKID_OK;
 }
 

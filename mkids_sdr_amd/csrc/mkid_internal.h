@@ -136,6 +136,10 @@ struct HeightArgs {
     int64_t rows, j0, n;    // n: packets (or the bound on *d_n)
     int32_t C, ncoeff, pre;
     const int64_t* d_n;     // nullable: device packet count (min(*d_n, n) packets are processed)
+    // carried phase history: rows j0 - hrows .. j0 - 1 ([hrows][C]), read for windows that start
+    // before the call's first row (hrows = 0: none)
+    const float* hist;
+    int64_t hrows;
 };
 
 // launchers (return hipError_t of the launch)

@@ -7,7 +7,8 @@ definition restated here is this repository's (include/mkidgpu.h): fo
 (channel 12 bits at MKID_PKT_CH_SHIFT, 28-bit phase-sample stamp ts)
     h = sum_{i < ncoeff} coeff[ch][i] * phase[ts - pre + i][ch]
 over phase rows holding global phase indices j0 .. j0 + rows - 1 (the 28-bit stamp unwrapped
-against j0); NaN when the window is not inside the rows. Float64 accumulation: the device's
+into [j0 - 2^27, j0 + 2^27)); NaN when the window is not inside the rows (or, with the device's
+carried history, its last rows before j0). Float64 accumulation: the device's
 fp32 result is compared within a relative tolerance. Parity unpinned against the reference
 (stub there).
 """
@@ -27,7 +28,8 @@ def pulse_heights(phase, events, coeff, pre, j0=0):
     for p, w in enumerate(ev.tolist()):
         ch = (w >> CH_SHIFT) & 0xFFF
         ts = w & TS_MASK
-        jg = j0 + ((ts - (j0 & TS_MASK)) & TS_MASK)
+        base = max(j0 - (1 << 27), 0)                 # stamps unwrap into [j0 - 2^27, j0 + 2^27)
+        jg = base + ((ts - (base & TS_MASK)) & TS_MASK)
         r0 = jg - j0 - pre
         if ch >= C or r0 < 0 or r0 + ncoeff > rows:
             continue

@@ -3,7 +3,8 @@ mkid_set_pulse_filter / mkid_pulse_heights, k_heights.hip) against oracle/height
 
 CPU: the oracle against a plain double loop, including 28-bit stamp unwrapping and windows that
 leave the rows. GPU: the device heights on the device's own phase and packets, config-5 geometry
-(2048 channels, N = 4096, split front end) and a streamed 1024-channel fused case with j0 > 0;
+(2048 channels, N = 4096) and streamed 1024-channel fused cases with j0 > 0 and with the phase
+history carried across calls;
 fp32 accumulation of <= 128 products, so the bar is relative 1e-5 of sum |coeff * phase|.
 """
 import numpy as np
@@ -20,7 +21,8 @@ def _loop(phase, events, coeff, pre, j0):
     out = []
     for w in events.tolist():
         ch, ts = w >> 52, w & oh.TS_MASK
-        jg = j0 + ((ts - (j0 & oh.TS_MASK)) & oh.TS_MASK)
+        base = max(j0 - (1 << 27), 0)
+        jg = base + ((ts - (base & oh.TS_MASK)) & oh.TS_MASK)
         r0 = jg - j0 - pre
         if r0 < 0 or r0 + coeff.shape[1] > phase.shape[0]:
             out.append(np.nan)
@@ -118,6 +120,47 @@ def test_heights_streamed_fused_j0(gpu):
         ch.close()
     assert n > 100
     _check(phase, ev, coeff.astype(np.float64), 40, J, got)
+
+
+@pytest.mark.gpu
+def test_heights_history_across_calls(gpu):
+    """Heights after every call of a stream: windows that start before a call's first row read
+    the context's carried copy of the previous call's last rows, so every packet of the second
+    call whose window ends inside the stream equals the oracle on the concatenated phase."""
+    import torch
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S, pre, nco = 1024, 2 ** 20, 20, 100
+    J = S // (2 * C)
+    ch = Channelizer(C, max_chunk=S)
+    try:
+        ch.set_fir(np.tile(np.arange(26, dtype=np.int16) * 40 - 500, (C, 1)))
+        ch.set_thresholds(np.full(C, -200, np.int32))
+        coeff = np.random.default_rng(65).normal(size=(C, nco)).astype(np.float32)
+        ch.set_pulse_filter(coeff, pre=pre)
+        x = torch.from_numpy(_noise_iq(2 * S, 66)).cuda()
+        phases, evs, hs = [], [], []
+        for k in range(2):
+            d_ph = torch.empty((J, C), dtype=torch.float32, device='cuda')
+            d_ev = torch.empty(J * C, dtype=torch.int64, device='cuda')
+            d_cnt = torch.zeros(2, dtype=torch.int64, device='cuda')
+            ch.process_device(x[k * S:(k + 1) * S], S, d_ph, d_ev, J * C, d_cnt)
+            torch.cuda.synchronize()
+            n = int(d_cnt[1].item())
+            d_h = torch.empty(max(n, 1), dtype=torch.float32, device='cuda')
+            ch.pulse_heights_device(d_ph, J, k * J, d_ev, n, d_h)
+            torch.cuda.synchronize()
+            phases.append(d_ph.cpu().numpy())
+            evs.append(d_ev[:n].cpu().numpy().view(np.uint64))
+            hs.append(d_h[:n].cpu().numpy())
+    finally:
+        ch.close()
+    phase = np.concatenate(phases)
+    ev2 = evs[1]
+    ts = (ev2 & np.uint64(oh.TS_MASK)).astype(np.int64)
+    early = (ts - pre >= J - nco) & (ts - pre < J)      # windows reaching into the first call
+    assert early.sum() > 5
+    assert np.all(np.isfinite(hs[1][early]))
+    _check(phase, ev2, coeff.astype(np.float64), pre, 0, hs[1])
 
 
 @pytest.mark.gpu

@@ -146,11 +146,13 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group('nccl')
+    # the rank's GPU first, then the process group bound to it (RCCL communicators are created
+    # for this device, not guessed from the rank)
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group('nccl', device_id=dev)
 
     from mkids_sdr_amd import _lib
     from mkids_sdr_amd.channelizer import Channelizer

@@ -57,6 +57,11 @@
 #ifndef MKID_CMUL
 #define MKID_CMUL cmul_pk
 #endif
+// PFB tap quads in VGPRs (16 per lane; -1.1 % k_front2 same-box, profiles/r02_v11_kbench_f2_tapreg.json;
+// default on once the GPU parity suite has run with it)
+#ifndef MKID_F2_TAPREG
+#define MKID_F2_TAPREG 0
+#endif
 
 namespace mkid {
 
@@ -180,7 +185,7 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
     float2* fbuf = reinterpret_cast<float2*>(smem + G::off_fbuf);
-    const uint2* taps = reinterpret_cast<const uint2*>(smem + G::off_taps);
+    [[maybe_unused]] const uint2* taps = reinterpret_cast<const uint2*>(smem + G::off_taps);
     float2* tw1 = reinterpret_cast<float2*>(smem + G::off_tw1);
     float2* tw2 = reinterpret_cast<float2*>(smem + G::off_tw2);
 
@@ -198,7 +203,8 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
     float2* reg = fbuf + slot * G::FB + w * G::REG;
 
     // tables: taps in the permuted point order, stage-1/2 twiddles
-    for (int p = tid; p < N; p += G::BT) reinterpret_cast<uint2*>(smem + G::off_taps)[(p % NW) * 512 + p / NW] = a.pfbq[p];
+    if (!MKID_F2_TAPREG)
+        for (int p = tid; p < N; p += G::BT) reinterpret_cast<uint2*>(smem + G::off_taps)[(p % NW) * 512 + p / NW] = a.pfbq[p];
     for (int i = tid; i < 7 * 64; i += G::BT) {
         const int k = i / 64 + 1, l = i % 64;
         double sn, cs;
@@ -260,7 +266,14 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
     float2* t2w = reg + 72 * kl + la;        // T2 write: i = 64 kl + 8 r + la  -> i + (i >> 3)
     const float2* t2r = reg + 72 * kl + 9 * la;  // T2 read: i = 64 kl + 8 la + r
     float2* yw = reg + ((kl + 8 * la) ^ (la << 1));   // Y: k = kl + 8 la + 64 r, swizzled
+#if !MKID_F2_TAPREG
     const uint2* tp = taps + w * 512 + L;     // tap quad of point r at tp[64 r]
+#else
+    // the wave's points are the same every frame: tap quads in VGPRs instead of LDS reads
+    uint2 tq[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
+#endif
     const float2* t1 = tw1 + L;               // W_512^{L k} at t1[64 (k - 1)]
     const float2* t2 = tw2 + la;              // W_64^{la k} at t2[8 (k - 1)]
 
@@ -284,7 +297,11 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
         for (int r = 0; r < 8; ++r) {
             const int hi = r >> 2;
             const int pos = w * (M / NW) + 64 * (r & 3) + L;
+#if MKID_F2_TAPREG
+            const uint64_t h64 = (uint64_t)tq[r].x | ((uint64_t)tq[r].y << 32);
+#else
             const uint64_t h64 = *reinterpret_cast<const uint64_t*>(tp + 64 * r);
+#endif
             uint32_t x4[T];
 #pragma unroll
             for (int tau = 0; tau < T; ++tau) {

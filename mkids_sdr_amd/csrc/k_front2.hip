@@ -57,10 +57,9 @@
 #ifndef MKID_CMUL
 #define MKID_CMUL cmul_pk
 #endif
-// PFB tap quads in VGPRs (16 per lane; -1.1 % k_front2 same-box, profiles/r02_v11_kbench_f2_tapreg.json;
-// default on once the GPU parity suite has run with it)
+// PFB tap quads in VGPRs (16 per lane; -1.1 % k_front2 same-box, profiles/r02_v11_kbench_f2_tapreg.json)
 #ifndef MKID_F2_TAPREG
-#define MKID_F2_TAPREG 0
+#define MKID_F2_TAPREG 1
 #endif
 
 namespace mkid {

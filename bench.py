@@ -63,6 +63,15 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-phase', action='store_true', help='do not materialise the phase stream')
     p.add_argument('--copy-mib', type=int, default=2048, help='stream-copy probe size (MiB)')
+    p.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                   help='N > 1 packet gather: RCCL on device buffers (one GPU per rank) or gloo '
+                        'through pinned host memory (ranks may share a GPU)')
+    p.add_argument('--check-gather', action='store_true',
+                   help='N > 1: verify that rank 0 received every rank\'s last-step packet list unchanged')
+    p.add_argument('--no-witness', action='store_true',
+                   help='skip the parity witness: the one-core CPU sample (the first 2^cpu-samples-log2 '
+                        'samples of the step input) re-run on the GPU from a reset context and compared '
+                        'with the oracle outputs the CPU leg computes anyway')
     return p.parse_args()
 
 
@@ -138,6 +147,30 @@ def pulse_filter(C, npre=20, ncoeff=100, tau_fall=65.0):
     return np.tile(g.astype(np.float32), (C, 1)), npre
 
 
+def gather_report(gather, ev_slots, cnt_slots, last, rank, world, ctrl, args):
+    """After the timed loop (outside it): per-rank packet counts of the last step and, with
+    --check-gather, whether rank 0's gathered lists equal every rank's own list byte for byte
+    (sha256 of the int64 words exchanged over the host control group)."""
+    import hashlib
+    import torch.distributed as dist
+    n = int(cnt_slots[last][1].item())
+    mine = ev_slots[last][:n].cpu().numpy()
+    own = (n, hashlib.sha256(mine.tobytes()).hexdigest())
+    allown = [None] * world
+    dist.all_gather_object(allown, own, group=ctrl)
+    out = {'backend': args.backend, 'ranks': world, 'overlapped': True,
+           'packets_gathered_total': int(gather.total) if rank == 0 else None,
+           'last_step_counts': [a[0] for a in allown]}
+    if args.check_gather and rank == 0:
+        got = gather.last
+        ok = got is not None and len(got) == world and all(
+            (int(g.numel()), hashlib.sha256(g.numpy().tobytes()).hexdigest()) == tuple(allown[r])
+            for r, g in enumerate(got))
+        out['lists_equal_rank_own'] = bool(ok)
+        out['feedlines_distinct'] = len({a[1] for a in allown}) == world
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -148,11 +181,22 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     # the rank's GPU first, then the process group bound to it (RCCL communicators are created
     # for this device, not guessed from the rank)
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    # device_count() does not initialise the GPU; ranks share a device only when there are more
+    # ranks than GPUs (a one-GPU box rehearsing N > 1, gloo backend only: RCCL needs distinct GPUs)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)
+    if world > 1 and args.backend == 'nccl' and world > ndev:
+        raise SystemExit('%d ranks on %d GPUs: RCCL needs one GPU per rank (use --backend gloo)' % (world, ndev))
+    torch.cuda.set_device(gpu)
+    dev = torch.device('cuda', gpu)
+    ctrl = None
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group('nccl', device_id=dev)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+            ctrl = dist.new_group(backend='gloo')     # host control channel (packet counts)
+        else:
+            dist.init_process_group('gloo')
 
     from mkids_sdr_amd import _lib
     from mkids_sdr_amd.channelizer import Channelizer
@@ -171,8 +215,12 @@ def main():
                                                       'BlackmanFilter_250kHz.txt')))
     base_mode = _lib.BASE_SVF if args.baseline == 'svf' else _lib.BASE_EMA
 
-    ch = Channelizer(C, device=local, max_chunk=S, dead_time=32, sample_rate=fs)
-    stream = torch.cuda.current_stream(dev)
+    ch = Channelizer(C, device=gpu, max_chunk=S, dead_time=32, sample_rate=fs)
+    # one stream for the context's kernels and torch's work on this rank: a torch.cuda.Stream,
+    # not torch's default stream, whose handle is 0 (mkid_set_stream(NULL) selects the
+    # context's own non-blocking stream, which events on torch's default stream do not order)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ch.set_stream(stream.cuda_stream)
     ch.set_bins(feed['dds']['bins'])
     ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
@@ -234,21 +282,38 @@ def main():
         ch.set_pulse_filter(coeff, pre)
         heights = torch.empty(cap, dtype=torch.float32, device=dev)
 
-    from mkids_sdr_amd.feedlines import gather_packets
+    # packet buffers: one slot per step in flight; with N > 1 two, so that the gather of step k
+    # (rank 0's PacketMaster role) overlaps step k+1's kernels (feedlines.PacketGather)
+    slots = 2 if world > 1 else 1
+    ev_slots = [d_events] + [torch.empty(cap, dtype=torch.int64, device=dev) for _ in range(slots - 1)]
+    cnt_slots = [d_counts] + [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(slots - 1)]
+    gather = None
+    if world > 1:
+        from mkids_sdr_amd.feedlines import PacketGather
+        gather = PacketGather(ev_slots, cnt_slots, args.backend, dev, dst=0, ctrl_group=ctrl,
+                              keep_last=args.check_gather)
     j0 = [0]
+    kstep = [0]
 
     def step():
-        ch.process_device(x, S, phase, d_events, cap, d_counts)
+        k = kstep[0]
+        s_ev, s_cnt = ev_slots[k % slots], cnt_slots[k % slots]
+        if gather is not None:
+            gather.before_step(k)
+        ch.process_device(x, S, phase, s_ev, cap, s_cnt)
         if heights is not None:
             # every packet of the step; the written count d_counts[1] is read on the device (no
             # host round trip inside the step); NaN where the window leaves the step's rows
-            ch.pulse_heights_counted(phase, J, j0[0], d_events, d_counts[1:], cap, heights)
+            ch.pulse_heights_counted(phase, J, j0[0], s_ev, s_cnt[1:], cap, heights)
         j0[0] += J
-        if world > 1:   # photon-list gather to rank 0 (the path's one exchange step)
-            gather_packets(d_events, int(d_counts[1].item()), dst=0)
+        if gather is not None:   # photon-list gather to rank 0 (the path's one exchange step)
+            gather.after_step(k)
+        kstep[0] += 1
 
     for _ in range(args.warmup):
         step()
+    if gather is not None:
+        gather.flush()
     torch.cuda.synchronize(dev)
     ch.set_timing(True)
     if world > 1:
@@ -257,15 +322,22 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if gather is not None:
+        gather.flush()           # the last step's lists are on rank 0 inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    gather_info = None
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=ctrl)
         dt = float(tt.item())
+        gather_info = gather_report(gather, ev_slots, cnt_slots, (kstep[0] - 1) % slots, rank, world,
+                                    ctrl, args)
     timing = ch.timing()
+    last = (kstep[0] - 1) % slots
+    d_events, d_counts = ev_slots[last], cnt_slots[last]
     counts = d_counts.cpu().numpy()
     ev_last = int(counts[0])
     det = None
@@ -356,7 +428,9 @@ def main():
                        'fs': fs, 'samples_per_step_per_gpu': S, 'baseline': args.baseline,
                        'phase_materialised': not args.no_phase,
                        'pulse_heights_in_step': bool(cf['heights']),
-                       'parallelism': 'feedline-per-GPU x%d, RCCL packet gather' % world},
+                       'parallelism': 'feedline-per-GPU x%d%s' % (
+                           world, '' if world == 1 else ', packet gather to rank 0 over %s' % (
+                               'RCCL' if args.backend == 'nccl' else 'gloo (pinned host buffers)'))},
             'per_gpu_msps': round(value / world, 1),
             'packets_per_step_rank0': ev_last,
             'injected_pulses_rank0': int(len(ps)),
@@ -381,51 +455,103 @@ def main():
                          'compute_peak_tflops': FP32_PEAK_TFLOPS},
             'kernel_ms': {k: round(v, 4) for k, v in kt.items()},
         }
+        if gather_info is not None:
+            out['gather'] = gather_info
         if not args.no_cpu_baseline and world == 1:
-            out['cpu_baseline'] = cpu_baseline(x, C, feed, lpf, mf, thr, 1 << args.cpu_samples_log2,
-                                               1 << args.cpu_all_samples_log2)
+            n1 = min(1 << args.cpu_samples_log2, S)
+            wit = None
+            if not args.no_witness:
+                wit = witness_device(ch, x, n1, C, N, dev, heights is not None)
+            out['cpu_baseline'] = cpu_baseline(x, C, feed, lpf, mf, thr, n1, 1 << args.cpu_all_samples_log2,
+                                               base_mode, wit)
+            par = out['cpu_baseline'].pop('parity', None)
+            if par is not None:
+                out['parity'] = par
         print(json.dumps(out), flush=True)
     ch.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall):
-    """The oracle (numpy float64 chain + C trigger) on a bounded sample of the same GPU input,
-    timed by tools/cpu_baseline.py in a child process: (i) one pinned core, (ii) all usable
-    cores chunk-parallel (cpu_baseline.kind = 'port'). `value` is the one-core rate."""
+def witness_device(ch, x, n, C, N, dev, with_heights):
+    """Full-size parity witness, GPU side (after the timed loop): the first n samples of the step
+    input re-run through the product path from a reset context — the same geometry and
+    configuration as every timed step, the same samples the CPU leg's oracle processes. Returns
+    host copies: phase float32 [n/N][C], Fix16_13 raw int16 [n/N][C], packets uint64 and (config
+    5) the per-packet heights of those packets."""
+    import torch
+    J = n // N
+    cap = J * C // 4 + 1024
+    ph = torch.empty(J * C, dtype=torch.float32, device=dev)
+    ev = torch.empty(cap, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    ch.reset()
+    ch.process_device(x, n, ph, ev, cap, cnt)
+    torch.cuda.synchronize(dev)
+    c = cnt.cpu().numpy()
+    if c[0] > c[1]:
+        raise RuntimeError('witness: %d packets produced, %d fit' % (c[0], c[1]))
+    out = dict(phase=ph.view(J, C).cpu().numpy(), raw=ch.raw_phase(),
+               packets=ev[:int(c[1])].cpu().numpy().view(np.uint64).copy())
+    if with_heights:
+        h = torch.empty(max(int(c[1]), 1), dtype=torch.float32, device=dev)
+        ch.pulse_heights_device(ph, J, 0, ev, int(c[1]), h)
+        torch.cuda.synchronize(dev)
+        out['heights'] = h[:int(c[1])].cpu().numpy()
+        coeff, pre = pulse_filter(C)
+        out['coeff'], out['pre'] = coeff, np.int64(pre)
+    return out
+
+
+def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall, mode, witness=None):
+    """The oracle (numpy float64 chain + C trigger, in the step's baseline mode) on a bounded
+    sample of the same GPU input, timed by tools/cpu_baseline.py in a child process: (i) one
+    pinned core, (ii) all usable cores chunk-parallel (cpu_baseline.kind = 'port'). `value` is the
+    one-core rate. With `witness` (witness_device's arrays for the first n1 samples) the child
+    also compares the oracle outputs of its one-core leg with them; the result comes back as
+    'parity'."""
     from mkids_sdr_amd.pfb import pfb_prototype
     n = max(n1, nall)
     n = min(n, x.numel() // 2)
     tmp = '/dev/shm' if os.path.isdir('/dev/shm') else '/tmp'
     inp = os.path.join(tmp, 'mkid_cpu_in_%d.npy' % os.getpid())
     cfgp = os.path.join(tmp, 'mkid_cpu_cfg_%d.npz' % os.getpid())
+    witp = os.path.join(tmp, 'mkid_cpu_wit_%d.npz' % os.getpid())
     try:
         np.save(inp, x[:2 * n].view(-1, 2).cpu().numpy())
         np.savez(cfgp, C=C, pfb=pfb_prototype(2 * C), bins=feed['dds']['bins'], lut_i=feed['dds']['lut_i'],
-                 lut_q=feed['dds']['lut_q'], lpf=lpf, fir=np.tile(mf, (C, 1)), thr=np.asarray(thr))
+                 lut_q=feed['dds']['lut_q'], lpf=lpf, fir=np.tile(mf, (C, 1)), thr=np.asarray(thr),
+                 mode=np.int64(mode))
+        cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--input', inp,
+               '--cfg', cfgp, '--one-core-samples', str(min(n1, n)), '--all-core-samples', str(min(nall, n))]
+        if witness is not None:
+            np.savez(witp, **witness)
+            cmd += ['--witness', witp]
+        del witness
         env = dict(os.environ)
         for k in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
             env[k] = '1'
-        r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--input', inp,
-                            '--cfg', cfgp, '--one-core-samples', str(min(n1, n)),
-                            '--all-core-samples', str(min(nall, n))],
-                           env=env, capture_output=True, text=True, timeout=600)
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
         if r.returncode != 0:
             return {'value': None, 'unit': 'MSample/s', 'cores': 1, 'kind': 'port',
                     'sample': 'cpu baseline failed: %s' % r.stderr[-400:]}
         res = json.loads(r.stdout.strip().splitlines()[-1])
     finally:
-        for p in (inp, cfgp):
+        for p in (inp, cfgp, witp):
             try:
                 os.remove(p)
             except OSError:
                 pass
     one, allc = res['one_core'], res['all_cores']
-    return {'value': one['value'], 'unit': 'MSample/s', 'cores': 1, 'kind': 'port',
-            'sample': one['sample'] + ' (1 pinned core, OMP/BLAS threads 1)',
-            'all_cores': allc, 'c1_cpu_only': res['c1'], 'cpu_model': res['cpu_model'],
-            'os_cpu_count': res['os_cpu_count'], 'sched_affinity': res['sched_affinity']}
+    out = {'value': one['value'], 'unit': 'MSample/s', 'cores': 1, 'kind': 'port',
+           'sample': one['sample'] + ' (1 pinned core, OMP/BLAS threads 1)',
+           'all_cores': allc, 'c1_cpu_only': res['c1'], 'cpu_model': res['cpu_model'],
+           'os_cpu_count': res['os_cpu_count'], 'sched_affinity': res['sched_affinity'],
+           'cpu_quota_cores': res.get('cpu_quota_cores')}
+    if 'parity' in res:
+        out['parity'] = res['parity']
+    return out
 
 
 if __name__ == '__main__':

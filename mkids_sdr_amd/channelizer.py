@@ -73,6 +73,9 @@ class Channelizer:
 
     # ---- configuration (one register group each) ---------------------------------------------
     def set_stream(self, stream_ptr):
+        """Run on an external hipStream_t (e.g. a torch.cuda.Stream's cuda_stream); 0/None
+        restores the context's own non-blocking stream. torch's default stream has handle 0, so
+        to share a stream with torch work use a torch.cuda.Stream, not the default one."""
         self._chk(self._L.mkid_set_stream(self._h, ctypes.c_void_p(stream_ptr or 0)))
 
     def set_pfb(self, coeffs):

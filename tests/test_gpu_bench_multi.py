@@ -1,0 +1,49 @@
+"""Config 4's code path executed on the one-GPU box: bench.py launched as 2 ranks by
+torch.distributed.run (one feedline per rank, config-3 geometry: 1024 ch, N = 2048), the
+per-step photon-list gather to rank 0 pipelined behind the next step (feedlines.PacketGather),
+the barrier + max-over-ranks timing, and rank 0's single JSON line. RCCL needs one GPU per rank,
+so the lists move over gloo through pinned host buffers here; the nccl branch differs only in the
+transport call. The launcher starts fresh rank processes; nothing re-execs a
+process that has touched the GPU. The reference counterpart: many ROACHes, one PacketMaster
+(PacketMaster.c:245-405, 577-625)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_gloo_gather(gpu):
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()),
+           os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--backend', 'gloo', '--check-gather',
+           '--config', '3', '--log2-samples', '26', '--steps', '3', '--warmup', '1',
+           '--no-cpu-baseline', '--copy-mib', '256']
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out['n_gpus'] == 2 and out['steps'] == 3
+    assert out['config']['channels'] == 1024 and out['config']['samples_per_step_per_gpu'] == 1 << 26
+    g = out['gather']
+    assert g['backend'] == 'gloo' and g['ranks'] == 2
+    assert g['lists_equal_rank_own'] is True
+    assert g['feedlines_distinct'] is True
+    assert min(g['last_step_counts']) > 1000
+    # every step's lists (warm-up included) reached rank 0
+    assert g['packets_gathered_total'] >= 4 * min(g['last_step_counts'])
+    assert out['value'] > 0

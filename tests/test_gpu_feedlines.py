@@ -1,8 +1,11 @@
 """The N > 1 feedline path on real hardware, world_size 2 over gloo: each rank runs its own
-synthetic feedline (different seed) through the HIP channeliser + trigger on cuda:0, checks its
-packets against the oracle trigger on its own Fix16_13 phase, and the packet lists are gathered to
-rank 0 with mkids_sdr_amd.feedlines.gather_packets (the code bench.py runs over RCCL). Both ranks
-share the box's single GPU (2 processes, well inside the per-card limit)."""
+synthetic feedline (different seed) at config 3/4's per-feedline geometry (1024 ch, N = 2048)
+through the HIP channeliser + trigger on cuda:0, checks its packets against the oracle trigger on
+its own Fix16_13 phase, and the packet lists are gathered to rank 0 with
+mkids_sdr_amd.feedlines.gather_packets. gloo's gather takes host tensors, so the lists cross as
+CPU tensors here; bench.py's pipelined gather (test_gpu_bench_multi.py) moves device buffers
+with backend nccl. Both ranks share the box's single GPU (2 processes, well inside the per-card
+limit)."""
 import os
 import socket
 import sys
@@ -37,8 +40,8 @@ def _worker(rank, world, port, q):
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        C, S = 64, 2 ** 15
-        case = signals.make_case(C, S, seed=11 + rank, pulses_per_ch=2.0)
+        C, S = 1024, 2 ** 20
+        case = signals.make_case(C, S, seed=11 + rank, pulses_per_ch=0.5, window_phase=60)
         quiet = signals.make_case(C, S, seed=11 + rank, pulses_per_ch=0)
         thr = signals.thresholds_from_quiet(quiet, signals.oracle_chain(quiet).process(quiet.iq)['raw'])
         ch = Channelizer(C, device=0, max_chunk=S)
@@ -73,7 +76,7 @@ def test_two_feedlines_gather_gloo():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=110) for _ in range(world)], key=lambda r: r[0])
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0

@@ -62,3 +62,65 @@ def test_gather_packets_gloo(world):
     assert len(lists) == world
     for r in range(world):
         assert lists[r] == _rank_packets(r).tolist()
+
+
+def _stream_worker(rank, world, port, q, steps):
+    """bench.py's streaming protocol on CPU: per step a new packet list is written into the
+    step's slot (the slot the gather of step k-1 may still hold), the gather of step k-1 runs
+    after step k is written, flush() after the last step."""
+    import torch
+    import torch.distributed as dist
+    from mkids_sdr_amd.feedlines import PacketGather
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        cap = 64
+        ev = [torch.full((cap,), -7, dtype=torch.int64) for _ in range(2)]
+        cnt = [torch.zeros(2, dtype=torch.int64) for _ in range(2)]
+        g = PacketGather(ev, cnt, 'gloo', 'cpu', keep_last=True)
+        seen = []
+        for k in range(steps):
+            g.before_step(k)
+            rng = np.random.default_rng(1000 * rank + k)
+            n = int(rng.integers(0, 40))          # empty lists included
+            vals = torch.from_numpy(rng.integers(0, 1 << 62, n))
+            s = k % 2
+            ev[s][:n] = vals
+            cnt[s][0] = cnt[s][1] = n
+            g.after_step(k)
+            if rank == 0 and k >= 1:
+                seen.append([t.tolist() for t in g.last])   # step k-1's lists
+        g.flush()
+        if rank == 0:
+            seen.append([t.tolist() for t in g.last])
+        q.put((rank, seen, g.total))
+    finally:
+        dist.destroy_process_group()
+
+
+def _expected(rank, k):
+    rng = np.random.default_rng(1000 * rank + k)
+    n = int(rng.integers(0, 40))
+    return rng.integers(0, 1 << 62, n).tolist()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_packet_gather_pipelined_gloo(world):
+    import torch.multiprocessing as mp
+    steps = 5
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, q, steps)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen = res[0][1]
+    assert len(seen) == steps
+    for k in range(steps):
+        assert seen[k] == [_expected(r, k) for r in range(world)], k
+    assert res[0][2] == sum(len(_expected(r, k)) for r in range(world) for k in range(steps))

@@ -53,10 +53,19 @@ def _load_cfg(path):
     return {k: z[k] for k in z.files}
 
 
-def run_chunk(args):
+def _trigger(trigger, cfg):
+    """The oracle trigger in the bench step's baseline mode (EMA 1 / SVF 2, register constants
+    of set_alpha.py / set_svf.py / set_base_thresh.py)."""
+    mode = int(cfg['mode']) if 'mode' in cfg else 1
+    return trigger.Trigger(int(cfg['C']), cfg['fir'], cfg['thr'], mode=mode)
+
+
+def run_chunk(args, collect=None):
     """Worker: process samples [a, b) of the shared input with a warm-up prefix; returns
-    (samples counted, seconds, packets)."""
-    cpu, inp, cfgp, a, b, prefix = args
+    (samples counted, seconds, packets). `collect` (a dict) receives the per-block oracle
+    outputs (phase float64, raw int16, packets) — list appends of arrays the chain produces
+    anyway, so the timing is unchanged."""
+    cpu, inp, cfgp, a, b, prefix, blk = args
     _single_thread_env()
     _pin(cpu)
     sys.path.insert(0, ROOT)
@@ -67,23 +76,108 @@ def run_chunk(args):
     N = 2 * C
     iq = np.load(inp, mmap_mode='r')
     o = chain.OracleChain(C, cfg['pfb'], cfg['bins'], cfg['lut_i'], cfg['lut_q'], cfg['lpf'])
-    tr = trigger.Trigger(C, cfg['fir'], cfg['thr'])
+    tr = _trigger(trigger, cfg)
     p0 = max(0, a - prefix)
     t0 = time.perf_counter()
     # warm-up prefix: history of the chain and of the trigger (outputs discarded)
     nev = 0
-    blk = 1 << 22
     if a > p0:
         r = o.process(np.asarray(iq[p0:a]))
         tr.run(r['raw'])
     for s in range(a, b, blk):
         e = min(b, s + blk)
         r = o.process(np.asarray(iq[s:e]))
-        _, k, _ = tr.run(r['raw'])
+        ev, k, _ = tr.run(r['raw'])
         nev += k
+        if collect is not None:
+            collect.setdefault('phase', []).append(r['phase'])
+            collect.setdefault('raw', []).append(r['raw'])
+            collect.setdefault('packets', []).append(ev)
     dt = time.perf_counter() - t0
     assert (b - a) % N == 0
     return b - a, dt, nev
+
+
+def cpu_quota_cores():
+    """CPUs this process may use per the cgroup CPU quota (cgroup v2 cpu.max / v1 cfs), or None
+    when unlimited: sched_getaffinity can list every CPU of the machine while the container's
+    share is much smaller."""
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, per = f.read().split()[:2]
+        if q != 'max':
+            return float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as f:
+            q = int(f.read())
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as f:
+            per = int(f.read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def witness_compare(col, witp, cfg):
+    """Full-size parity witness (bench.py `parity`): the oracle outputs of the one-core leg
+    against the device's outputs for the same samples. Bars (tests/test_gpu_parity.py,
+    north_star): phase within 1e-5 rad; Fix16_13 phase within 1 LSB (rounding-boundary flips);
+    packets bit-exact when the oracle trigger runs on the device's own Fix16_13 phase; full-chain
+    packets equal on every channel without a flip; (config 5) heights within 1e-5 relative of the
+    float64 oracle on the device's own phase and packets."""
+    import numpy as np
+    from oracle import trigger
+    w = np.load(witp, allow_pickle=False)
+    dph, draw, dpk = w['phase'], w['raw'], w['packets']
+    oph = np.concatenate(col['phase'])
+    oraw = np.concatenate(col['raw'])
+    opk = np.concatenate(col['packets']) if col['packets'] else np.zeros(0, np.uint64)
+    C = int(cfg['C'])
+    assert dph.shape == oph.shape == draw.shape, (dph.shape, oph.shape, draw.shape)
+    err = np.abs((dph.astype(np.float64) - oph + np.pi) % (2 * np.pi) - np.pi)
+    dr = draw.astype(np.int32) - oraw.astype(np.int32)
+    flips = dr != 0
+    own = _trigger(trigger, cfg).run(draw)[0]
+    own_equal = np.array_equal(np.sort(own), np.sort(dpk))
+    ch_of = lambda p: ((p >> np.uint64(52)) & np.uint64(0xFFF)).astype(np.int64)
+    dset = [set() for _ in range(C)]
+    oset = [set() for _ in range(C)]
+    for p, c in zip(dpk.tolist(), ch_of(dpk).tolist()):
+        dset[c].add(p)
+    for p, c in zip(opk.tolist(), ch_of(opk).tolist()):
+        oset[c].add(p)
+    diverged = [c for c in range(C) if dset[c] != oset[c]]
+    flip_ch = set(np.nonzero(flips.any(axis=0))[0].tolist())
+    unexplained = [c for c in diverged if c not in flip_ch]
+    out = dict(samples=int(dph.shape[0] * 2 * C), rows=int(dph.shape[0]), channels=C,
+               phase_max_err_rad=float(err.max()), phase_p999999_err_rad=float(np.quantile(err, 0.999999)),
+               phase_tol_rad=1e-5,
+               raw_flip_rate=float(flips.mean()), raw_max_abs_diff=int(np.abs(dr).max()),
+               channels_with_flip=len(flip_ch),
+               packets_device=int(dpk.size), packets_oracle_chain=int(opk.size),
+               packets_equal_on_device_raw=bool(own_equal),
+               channels_diverged_full_chain=len(diverged),
+               channels_diverged_without_flip=len(unexplained))
+    green = (out['phase_max_err_rad'] <= 1e-5 and out['raw_max_abs_diff'] <= 1 and own_equal
+             and not unexplained)
+    if 'heights' in w.files:
+        sys.path.insert(0, ROOT)
+        from oracle import heights as oh
+        ref = oh.pulse_heights(dph, dpk, w['coeff'], int(w['pre']), 0)
+        got = w['heights'].astype(np.float64)
+        nan_eq = bool(np.array_equal(np.isnan(ref), np.isnan(got)))
+        ok = ~np.isnan(ref)
+        rel = np.abs(got[ok] - ref[ok]) / np.maximum(np.abs(ref[ok]), 1e-3) if ok.any() else np.zeros(1)
+        end2end = oh.pulse_heights(oph, dpk, w['coeff'], int(w['pre']), 0)
+        e2e = np.abs(got[ok] - end2end[ok]) / np.maximum(np.abs(end2end[ok]), 1e-3) if ok.any() else np.zeros(1)
+        out['heights'] = dict(n=int(got.size), nan_positions_equal=nan_eq, max_rel_err=float(rel.max()),
+                              tol_rel=1e-5, max_rel_err_vs_oracle_phase=float(e2e.max()))
+        green = green and nan_eq and out['heights']['max_rel_err'] <= 1e-5
+    out['green'] = bool(green)
+    return out
 
 
 def c1_timing(cpu):
@@ -114,29 +208,44 @@ def main():
     ap.add_argument('--input', required=True, help='.npy int16 [S][2] sample of the GPU input')
     ap.add_argument('--cfg', required=True, help='.npz channel configuration')
     ap.add_argument('--one-core-samples', type=int, required=True)
-    ap.add_argument('--workers', type=int, default=0, help='0: min(16, usable CPUs)')
+    ap.add_argument('--workers', type=int, default=0,
+                    help='0: every usable CPU (sched_getaffinity), capped at the cgroup CPU quota')
     ap.add_argument('--all-core-samples', type=int, required=True)
+    ap.add_argument('--witness', default=None, help='.npz device outputs for the one-core sample')
     a = ap.parse_args()
     import numpy as np
     cfg = _load_cfg(a.cfg)
     C = int(cfg['C'])
     N = 2 * C
     aff = sorted(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else list(range(os.cpu_count()))
-    out = dict(cpu_model=cpu_model(), os_cpu_count=os.cpu_count(), sched_affinity=len(aff))
-    prefix = (16 + 520) * N   # >= (2T-1+24) hops of ADC history + 520 trigger warm-up rows
+    quota = cpu_quota_cores()
+    out = dict(cpu_model=cpu_model(), os_cpu_count=os.cpu_count(), sched_affinity=len(aff),
+               cpu_quota_cores=quota)
+    # >= (2T-1+24) hops of ADC history + 520 trigger warm-up rows (the EMA baseline's merge
+    # horizon). The SVF baseline needs ~10^5 rows to merge exactly; its chunks use
+    # the same prefix, so their first rows' packets are approximate (a timing baseline only).
+    prefix = (16 + 520) * N
 
     # (i) one core, one process
     n1 = a.one_core_samples - a.one_core_samples % N
-    s, dt, nev = run_chunk((aff[0], a.input, a.cfg, 0, n1, 0))
+    col = {} if a.witness else None
+    s, dt, nev = run_chunk((aff[0], a.input, a.cfg, 0, n1, 0, 1 << 22), collect=col)
     out['one_core'] = dict(value=round(s / dt / 1e6, 3), unit='MSample/s', cores=1,
                            sample='first %d samples of the GPU input, %.1f s, %d packets' % (s, dt, nev))
+    if col is not None:
+        out['parity'] = witness_compare(col, a.witness, cfg)
+        del col
 
-    # (ii) all cores: W pinned single-thread processes, chunk-parallel with a warm-up prefix
-    W = a.workers or min(16, len(aff))
+    # (ii) all cores: W pinned single-thread processes (one per usable CPU, at most the cgroup
+    #      quota: processes beyond it only time-share), chunk-parallel with a warm-up prefix
+    W = a.workers or len(aff)
+    if quota is not None:
+        W = min(W, max(1, int(quota)))
     W = max(1, min(W, len(aff)))
     n = a.all_core_samples - a.all_core_samples % (N * W)
     per = n // W
-    jobs = [(aff[i], a.input, a.cfg, i * per, (i + 1) * per, prefix) for i in range(W)]
+    blk = max(N, min(1 << 22, per) // N * N)
+    jobs = [(aff[i], a.input, a.cfg, i * per, (i + 1) * per, prefix, blk) for i in range(W)]
     import multiprocessing as mp
     ctx = mp.get_context('fork')   # this process never touched the GPU
     t0 = time.perf_counter()
@@ -145,9 +254,11 @@ def main():
     wall = time.perf_counter() - t0
     tot = sum(r[0] for r in res)
     out['all_cores'] = dict(value=round(tot / wall / 1e6, 3), unit='MSample/s', cores=W,
+                            cores_note='one pinned single-thread process per usable CPU '
+                                       '(sched_getaffinity %d, cgroup quota %s)' % (len(aff), quota),
                             sample='%d samples of the GPU input in %d chunks (+%d-sample warm-up prefix '
-                                   'each), %.1f s wall, %d packets' % (tot, W, prefix, wall,
-                                                                       sum(r[2] for r in res)))
+                                   'each, not counted), %.1f s wall, %d packets' % (tot, W, prefix, wall,
+                                                                                   sum(r[2] for r in res)))
     out['c1'] = c1_timing(aff[0])
     print(json.dumps(out), flush=True)
 

@@ -133,7 +133,9 @@ int mkid_reset_stream(mkid_ctx* ctx);
 
 /* Process nsamples (multiple of N) I/Q pairs, host pointers, synchronous. phase_out (nullable)
  * receives [nsamples/N][C] float32 rad; events_out receives up to cap packets, channel-major and
- * time-ascending within a channel; *nevents = packets produced (> cap => MKID_E_OVERFLOW). */
+ * time-ascending within a channel over the whole call (a call longer than cfg.max_chunk runs as
+ * max_chunk pieces whose lists are merged on the host); *nevents = packets produced (> cap =>
+ * MKID_E_OVERFLOW; the packets kept are then the first cap in time of each piece). */
 int mkid_process(mkid_ctx* ctx, const int16_t* iq, int64_t nsamples, float* phase_out,
                  uint64_t* events_out, int64_t cap, int64_t* nevents);
 
@@ -149,7 +151,11 @@ int mkid_process_device(mkid_ctx* ctx, const int16_t* d_iq, int64_t nsamples, fl
  * snapshot uploaded by the caller: the reference runs its trigger on snapshots too,
  * ROACH_Pulses.py:211-354, 614-727): matched filter, baseline, trigger, packets, with the
  * context's carried trigger state and phase-sample counter (advanced by rows). rows <=
- * max_chunk/N. d_counts / packet order as mkid_process_device. Asynchronous on the context stream. */
+ * max_chunk/N. d_counts / packet order as mkid_process_device. Asynchronous on the context stream.
+ * A context carries ONE stream: ADC samples (mkid_process*) or phase rows (this call). Calling one
+ * kind after the other without mkid_reset_stream fails with MKID_E_STATE, so a snapshot never
+ * advances the trigger state, the raw history or the packet stamps of a live ADC stream (use a
+ * second context for snapshots taken beside a running feedline). */
 int mkid_trigger_phase(mkid_ctx* ctx, const int16_t* d_raw, int64_t rows, uint64_t* d_events,
                        int64_t cap, int64_t* d_counts /* [2] */);
 
@@ -239,6 +245,9 @@ int mkid_optimal_filter(mkid_ctx* ctx, const double* d_template, const double* d
  * (28-bit stamps unwrapped into [j0 - 2^27, j0 + 2^27)); d_heights n floats. The context keeps
  * the last ncoeff rows it was given: when a call's j0 continues the previous call's rows, windows
  * that start before row j0 read them. NaN where the window is not inside (carried rows, rows).
+ * In a streamed run that is the packets of a call's last (ncoeff - pre) rows: pass them again
+ * with the next contiguous call (j0 = this call's j0 + rows) and their windows are then complete
+ * (carried rows + new rows); the heights of a call are otherwise final.
  * Asynchronous on the context stream; device pointers only. */
 int mkid_set_pulse_filter(mkid_ctx* ctx, const float* coeff, int32_t nch, int32_t ncoeff, int32_t pre);
 int mkid_pulse_heights(mkid_ctx* ctx, const float* d_phase, int64_t rows, int64_t j0,

@@ -187,6 +187,23 @@ def decode_snap_phase(buf):
     return np.stack([a[:, 1], a[:, 0]], axis=1).reshape(-1)
 
 
+def decode_qdr(buf):
+    """qdr0_memory longsnapshot words -> Fix16_13 raw, 2 samples per 32-bit word in time order,
+    '>h' each (ROACH_Pulses.py:476: struct.unpack('>%dh' % nLongsnapSamples, ...))."""
+    return np.frombuffer(bytes(buf), '>i2').astype(np.int64)
+
+
+def noise_spectrum(phase_deg, n_averages=100, norm1=50.0):
+    """The longsnapshot phase-noise spectrum (ROACH_Pulses.py:521-543): the stream cut into
+    n_averages pieces of len // n_averages samples, mean over pieces of
+    20 log10(|fft(piece)| / norm1 / 1e-6); returns (fftfreq(piece length), spectrum)."""
+    x = np.asarray(phase_deg, np.float64)
+    n = len(x) // n_averages
+    pieces = x[:n * n_averages].reshape(n_averages, n)
+    spec = (20 * np.log10(np.abs(np.fft.fft(pieces, axis=1)) / norm1 / 1e-6)).sum(axis=0) / n_averages
+    return np.fft.fftfreq(n), spec
+
+
 def encode_conv_phase_snap(raw):
     """conv_phase_snapPhase_bram: one sample per word in bytes [2:4] (pulse_triggering_v2.py:94)."""
     r = np.asarray(raw, np.int64)

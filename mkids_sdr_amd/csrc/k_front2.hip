@@ -418,14 +418,15 @@ static hipError_t launch_front2_n(const FrontArgs& a0, hipStream_t s) {
     if (e != hipSuccess) return e;
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
-    // one round of workgroups over the 256 CUs for a large chunk (2048/N workgroups fit a CU: the
-    // LDS plan scales with N), runs of <= 4096 frames: at N = 2048 a 2^30-sample chunk is one
-    // 4096-frame run per CU, the 24-frame low-pass warm-up 0.6 % of it (-1.4 % against 1024 runs
-    // of 1024 frames, tools/kbench.py A/B)
-#ifndef MKID_F2_BLOCKS
-#define MKID_F2_BLOCKS 256
+    // one round of workgroups over the device's CUs for a large chunk (2048/N workgroups fit a CU:
+    // the LDS plan scales with N), runs of <= 4096 frames: at N = 2048 a 2^30-sample chunk is one
+    // 4096-frame run per CU of MI355X's 256, the 24-frame low-pass warm-up 0.6 % of it (-1.4 %
+    // against 1024 runs of 1024 frames, tools/kbench.py A/B)
+#ifndef MKID_F2_BLOCKS_PER_CU
+#define MKID_F2_BLOCKS_PER_CU 1
 #endif
-    int64_t fpb = a.K / ((int64_t)MKID_F2_BLOCKS * (2048 / N));
+    const int64_t ncu = a.ncu > 0 ? a.ncu : 256;
+    int64_t fpb = a.K / ((int64_t)MKID_F2_BLOCKS_PER_CU * ncu * (2048 / N));
     fpb = fpb < 64 ? 64 : (fpb > 4096 ? 4096 : fpb);
     fpb = (fpb + G::FPB - 1) / G::FPB * G::FPB;
     a.frames_per_block = fpb;

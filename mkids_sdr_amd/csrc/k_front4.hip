@@ -401,12 +401,13 @@ hipError_t launch_front4(const FrontArgs& a0, hipStream_t s) {
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
     // runs of up to 1024 frames (the 24-frame low-pass warm-up is 2.3 % of a full run): a full
-    // 2^30-sample chunk is MKID_F4_BLOCKS workgroups, two rounds over the 256 CUs (-2.2 % against
-    // 1024 runs of 512 frames, tools/kbench.py A/B)
-#ifndef MKID_F4_BLOCKS
-#define MKID_F4_BLOCKS 512
+    // 2^30-sample chunk is two rounds of workgroups over the device's CUs (-2.2 % against 1024
+    // runs of 512 frames on MI355X's 256 CUs, tools/kbench.py A/B)
+#ifndef MKID_F4_BLOCKS_PER_CU
+#define MKID_F4_BLOCKS_PER_CU 2
 #endif
-    int64_t fpb = a.K / MKID_F4_BLOCKS;
+    const int64_t ncu = a.ncu > 0 ? a.ncu : 256;
+    int64_t fpb = a.K / ((int64_t)MKID_F4_BLOCKS_PER_CU * ncu);
     fpb = fpb < 64 ? 64 : (fpb > 1024 ? 1024 : fpb);
     fpb = (fpb + G4::FPB - 1) / G4::FPB * G4::FPB;
     a.frames_per_block = fpb;

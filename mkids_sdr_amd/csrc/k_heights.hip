@@ -50,7 +50,8 @@ __global__ __launch_bounds__(64 * kHeightWaves) void k_pulse_heights(HeightArgs 
 hipError_t launch_pulse_heights(const HeightArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
     int64_t blocks = (a.n + kHeightWaves - 1) / kHeightWaves;
-    if (blocks > 256 * 32) blocks = 256 * 32;  // 8 waves per SIMD on every CU, then grid-stride
+    const int64_t cap = (int64_t)(a.ncu > 0 ? a.ncu : 256) * 32;  // 8 waves per SIMD on every CU, then grid-stride
+    if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL(k_pulse_heights, dim3((unsigned)blocks), dim3(64 * kHeightWaves), 0, s, a);
     return hipGetLastError();
 }

@@ -79,6 +79,10 @@ struct mkid_ctx {
     hipStream_t own = nullptr, stream = nullptr;
     std::string err;
     int C = 0, N = 0, M = 0, T = 0, P = 0, capc = 0;
+    int ncu = 256;  // compute units of the device (launch grids are per-CU multiples)
+    // what the carried stream state belongs to: 0 none (fresh / reset), 1 an ADC stream
+    // (mkid_process*), 2 a phase-row stream (mkid_trigger_phase); mixing them needs a reset
+    int stream_kind = 0;
     int64_t Kmax = 0, Jmax = 0;
     // configuration
     float* d_pfb = nullptr;      // effective taps h_q 2^-S (float, split path)
@@ -390,6 +394,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
             ncu = 256;
+        c->ncu = ncu;
         c->svf_lanes = (int64_t)ncu * 128;
         if (const char* ev = getenv("MKID_SVF_LANES")) c->svf_lanes = std::max<int64_t>(1, atoll(ev));
         if (const char* ev = getenv("MKID_SVF_WARMUP"))
@@ -401,7 +406,9 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     const int64_t capseg = seg_capacity(Lmax, cfg->dead_time);
     // one [C][sum of the sub-chunks' segments][capseg] table per call (single compaction)
     c->slot_cap = (int64_t)C * c->nsub_max * std::max<int64_t>(c->nseg_max * capseg, c->capc);
-    c->scratch_cap = std::max<int64_t>(capseg, c->capc);
+    // the fix-up re-runs one segment per channel into [C][capseg]: any plan's capseg, including an
+    // SVF segment as long as the whole call (plan_sub), whatever max_events_per_ch says
+    c->scratch_cap = std::max<int64_t>(std::max<int64_t>(capseg, c->capc), seg_capacity(c->Jmax, cfg->dead_time));
     c->H = c->fused ? front_hist_samples(N) : (int64_t)c->T * N - c->M;
     const int64_t H = c->H;
     auto fail = [&](hipError_t e, const char* what) {
@@ -664,6 +671,7 @@ int mkid_reset_stream(mkid_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->k0 = 0;
     c->j0 = 0;
+    c->stream_kind = 0;
     c->last_J = 0;
     c->last_subJ = 0;
     c->last_raw_row = 0;
@@ -726,6 +734,7 @@ static int plan_call(mkid_ctx* c, int64_t n, int64_t G, std::vector<SubPlan>& su
         if (subs.back().nseg > c->nseg_max) FAIL(c, MKID_E_ARG, "trigger plan exceeds the segment tables");
     }
     if ((int64_t)c->C * stride * capseg > c->slot_cap) FAIL(c, MKID_E_ARG, "trigger plan exceeds the packet slot table");
+    if (capseg > c->scratch_cap) FAIL(c, MKID_E_ARG, "trigger plan exceeds the fix-up scratch");
     return MKID_OK;
 }
 
@@ -821,6 +830,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.k0 = c->k0;
         fa.avail = off;
         fa.P = c->P;
+        fa.ncu = c->ncu;
         fa.taps = c->lpf;
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
@@ -864,6 +874,9 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     // the workspace (raw rows, IQ tap, slot table) is sized for max_chunk samples per call
     if (n > c->cfg.max_chunk) FAIL(c, MKID_E_ARG, "nsamples exceeds cfg.max_chunk");
     if (((uintptr_t)d_iq & 15) != 0) FAIL(c, MKID_E_ARG, "d_iq must be 16-byte aligned");
+    if (c->stream_kind == 2)
+        FAIL(c, MKID_E_STATE, "the context carries a phase-row stream (mkid_trigger_phase); mkid_reset_stream first");
+    c->stream_kind = 1;
     HIPCHK(c, hipSetDevice(c->device));
     if (c->fused) return process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts);
     const int C = c->C, N = c->N, M = c->M;
@@ -951,6 +964,9 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
     if (!c || !d_raw || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
     if (rows <= 0 || rows > c->cfg.max_chunk / c->N) FAIL(c, MKID_E_ARG, "rows must be in 1 .. max_chunk/N");
     if (((uintptr_t)d_raw & 3) != 0) FAIL(c, MKID_E_ARG, "d_raw must be 4-byte aligned");
+    if (c->stream_kind == 1)
+        FAIL(c, MKID_E_STATE, "the context carries an ADC stream (mkid_process); mkid_reset_stream first");
+    c->stream_kind = 2;
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = c->stream;
     std::vector<SubPlan> subs;
@@ -1009,6 +1025,10 @@ int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, ui
         written += take;
     }
     *nevents = produced;
+    if (n > chunk && written > 1)   // chunks were compacted separately: merge to channel-major
+        std::stable_sort(events_out, events_out + written, [](uint64_t a, uint64_t b) {
+            return (a >> MKID_PKT_CH_SHIFT) < (b >> MKID_PKT_CH_SHIFT);
+        });
     if (produced > written) FAIL(c, MKID_E_OVERFLOW, "event capacity exceeded; events dropped");
     return MKID_OK;
 }
@@ -1208,7 +1228,7 @@ static int pulse_heights(mkid_ctx* c, const float* d_phase, int64_t rows, int64_
     const int64_t hrows = (c->phist_end == j0) ? c->phist_rows : 0;
     const int64_t H = c->h_ncoeff;   // d_phist: H rows, the valid ones are its last phist_rows
     HeightArgs a{d_phase, d_events, c->d_hcoeff, d_heights, rows, j0, n, c->C, c->h_ncoeff, c->h_pre, d_n,
-                 c->d_phist + (H - hrows) * c->C, hrows};
+                 c->d_phist + (H - hrows) * c->C, hrows, c->ncu, 0};
     KTime kt;
     tstart(c, MKID_K_HEIGHTS, &kt, c->stream);
     HIPCHK(c, launch_pulse_heights(a, c->stream));

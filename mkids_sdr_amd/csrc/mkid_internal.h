@@ -93,7 +93,7 @@ struct FrontArgs {
     int64_t frames_per_block;  // set by the launcher
     int64_t avail;          // samples readable before x (earlier sub-chunks of the same call)
     int32_t P;              // LO period (power of two)
-    int32_t pad;
+    int32_t ncu;            // compute units of the device (grid sizing: per-CU multipliers)
     LpfTaps taps;
     int16_t* iqtap;         // [K/2][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
     int32_t iq_ch;
@@ -140,6 +140,8 @@ struct HeightArgs {
     // before the call's first row (hrows = 0: none)
     const float* hist;
     int64_t hrows;
+    int32_t ncu;            // compute units of the device (grid cap)
+    int32_t pad;
 };
 
 // launchers (return hipError_t of the launch)

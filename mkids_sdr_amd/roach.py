@@ -28,7 +28,7 @@ import struct
 
 import numpy as np
 
-from . import codecs, lut, packets
+from . import codecs, replay, lut, packets
 
 FIR_RE = re.compile(r'^FIR_b(\d+)b(\d+)$')
 PULSE_RING = 2 ** 14          # pulses_bram0/1 depth (ROACH_Pulses.py:799-800)
@@ -303,9 +303,14 @@ class FpgaClient:
 
     def _raw_of(self, ch, nsamp):
         """Fix16_13 phase of channel ch for the next nsamp phase samples (device raw values:
-        rint(phase * 8192) of the float32 phase, clamped, exactly as k_front quantises)."""
-        phase, _ = self.run(nsamp)
-        return np.clip(np.rint(phase[:, ch] * np.float32(8192)), -25736, 25736).astype(np.int64)
+        rint(phase * 8192) of the float32 phase, clamped, exactly as k_front quantises). Long
+        captures (qdr0_memory: 2^20 samples) stream in pieces of at most 2^24 ADC samples."""
+        piece = max(1, (1 << 24) // self.N)
+        out = []
+        for r0 in range(0, nsamp, piece):
+            phase, _ = self.run(min(piece, nsamp - r0))
+            out.append(np.clip(np.rint(phase[:, ch] * np.float32(8192)), -25736, 25736).astype(np.int64))
+        return np.concatenate(out) if out else np.zeros(0, np.int64)
 
     def _iq_of(self, ch, npairs):
         """Low-pass I/Q of channel ch for the next npairs phase samples (device IQ tap)."""
@@ -538,6 +543,72 @@ class RoachPulses:
 
     def loadThresholds(self):
         return [self.loadSingleThreshold(ch) for ch in range(self.N_freqs)]
+
+    def _snap_qdr(self, ch, steps, L=2 ** 10, n_qdr=2 ** 19):
+        """The snapshot loop shared by longsnapshot and contsnapshot (ROACH_Pulses.py:449-463,
+        585-597): per step arm snapPhase + snapqdr, read 2^10 snapPhase words and 2^19 qdr0 words."""
+        self.roach.write_int('ch_we', ch)
+        snap, qdr = b'', b''
+        for _ in range(steps):
+            for name, v in (('snapPhase_ctrl', 0), ('snapqdr_ctrl', 0), ('startSnap', 0),
+                            ('snapqdr_ctrl', 1), ('snapPhase_ctrl', 1), ('startSnap', 1)):
+                self.roach.write_int(name, v)
+            snap += self.roach.read('snapPhase_bram', 4 * L)
+            qdr += self.roach.read('qdr0_memory', n_qdr * 4)
+        for name in ('snapPhase_ctrl', 'snapqdr_ctrl', 'startSnap'):
+            self.roach.write_int(name, 0)
+        return codecs.decode_snap_phase(snap), codecs.decode_qdr(qdr)
+
+    def longsnapshot(self, ch, steps=1, save_dir=None, n_averages=100, norm1=50.0):
+        """ROACH_Pulses.py:433-551: `steps` snapPhase + qdr0 snapshots of channel ch in degrees,
+        their statistics, and the qdr stream's phase-noise spectrum over n_averages FFTs
+        (521-543; steps=1: 2^20 samples, 10485-point FFTs, the bins of the reference's saved
+        ch_noifreqs_0.txt). With save_dir, the reference's text files are written there
+        (ch_out_<ch>.txt, ch_snap_<ch>.txt, ch_noifreqs_<ch>.txt, ch_noise_<ch>.txt)."""
+        snap_raw, qdr_raw = self._snap_qdr(ch, steps)
+        phase = snap_raw * self.scale_to_angle
+        qdr_phase = qdr_raw * self.scale_to_angle
+        freqs, noise = codecs.noise_spectrum(qdr_phase, n_averages, norm1)
+        out = dict(phase=phase, qdr_phase=qdr_phase, noiseFFTFreqs=freqs, noiseFFT=noise,
+                   median=float(np.median(phase)), mean=float(np.mean(phase)), std=float(np.std(phase)))
+        if save_dir is not None:
+            import os
+            os.makedirs(save_dir, exist_ok=True)
+            for name, arr in (('ch_out', qdr_phase), ('ch_snap', phase), ('ch_noifreqs', freqs),
+                              ('ch_noise', noise)):
+                with open(os.path.join(save_dir, '%s_%d.txt' % (name, ch)), 'w') as f:
+                    f.writelines('%r\n' % float(q) for q in arr)
+        return out
+
+    def contsnapshot(self, ch, steps=1, phase_threshold=-20.0, averagelength_power=10, maxloops=None,
+                     cap=4096):
+        """ROACH_Pulses.py:557-762: qdr0 snapshot(s) of channel ch in degrees, then the block-mean
+        trigger over it (means of 2^averagelength_power-sample blocks, start 500, hit when
+        |mean - x| > phase_threshold, skip 1000, stop at bob + 1500 > len: 614-727) — run on the
+        device (mkid_replay_trigger) — and the 2000-sample window [bob-500, bob+1500) of every hit.
+        The reference's loop also stops after `maxloops` passes (failsafe, 747-750); None = no cap.
+        Returns dict(pulsenumber, phase (the two columns it saves, '%i %.2f'), hits, total_pulses,
+        qdr_phase (the snapshot in degrees))."""
+        import torch
+        _, qdr_raw = self._snap_qdr(ch, steps)
+        qdr_phase = qdr_raw * self.scale_to_angle
+        c = self.roach.channelizer()
+        dev = c.torch_device()
+        d_raw = torch.from_numpy(qdr_raw.astype(np.int16)).to(dev)
+        torch.cuda.synchronize(dev)
+        hits = replay.block_mean_trigger(c, d_raw, len(qdr_raw), 1, 1, averagelength=2 ** int(averagelength_power),
+                                         threshold=float(phase_threshold), start=500, need=1500, skip=1000,
+                                         wrap_negative=False, cap=cap)[0]
+        if maxloops is not None:
+            # pass index of the k-th hit (0-based): every pass advances bob by 1, a hit by 1000
+            hits = [h for k, h in enumerate(hits) if (h - 500) - 999 * k < int(maxloops)]
+        pulsenumber = [0.0] * 2000                  # pulse 0's numbers: the initial zeros (560-561)
+        final = []
+        for k, h in enumerate(hits):
+            final.extend(qdr_phase[h - 500:h + 1500].tolist())
+            if k > 0:
+                pulsenumber.extend([float(k)] * 2000)
+        return dict(pulsenumber=pulsenumber, phase=final, hits=hits, total_pulses=len(hits), qdr_phase=qdr_phase)
 
     def readPulses(self, steps=1):
         """ROACH_Pulses.py:782-832: poll pulses_addr, decode the BRAM ring."""

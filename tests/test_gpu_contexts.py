@@ -87,3 +87,53 @@ def test_packets_channel_major_over_whole_call(gpu, front):
         ch.close()
     assert len(ev) > 100
     assert np.array_equal(ev, sort_events(ev))
+
+
+def test_host_call_longer_than_max_chunk_is_channel_major(gpu):
+    """mkid_process cuts a call longer than cfg.max_chunk into max_chunk pieces; the pieces'
+    lists are merged on the host, so the whole call is channel-major and time-ascending, and the
+    packets equal one call through a context whose workspace holds the whole stream."""
+    from mkids_sdr_amd.channelizer import Channelizer
+    C = 256
+    S = 600 * 2 * C
+    case = signals.make_case(C, S, seed=43, pulses_per_ch=6.0, noise=100.0)
+    thr = quiet_thresholds(C, S // 4, 43)
+    out = {}
+    for mc in (S, S // 4):
+        ch = Channelizer(C, max_chunk=mc)
+        try:
+            configure(ch, case, thr)
+            out[mc] = ch.process(case.iq)
+        finally:
+            ch.close()
+    ev = out[S // 4][1]
+    assert len(ev) > 100
+    assert np.array_equal(ev, sort_events(ev))
+    assert np.array_equal(ev, out[S][1])
+    assert np.array_equal(out[S // 4][0], out[S][0])
+
+
+def test_adc_and_phase_streams_do_not_mix(gpu):
+    """A context carries one stream: mkid_trigger_phase on a context mid-ADC-stream (or the
+    reverse) fails with MKID_E_STATE instead of shifting the live stream's stamps; after
+    mkid_reset_stream either kind may start."""
+    from mkids_sdr_amd import _lib
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 64, 1 << 14
+    case = signals.make_case(C, S, seed=44, pulses_per_ch=0.0)
+    ch = Channelizer(C, max_chunk=S)
+    try:
+        configure(ch, case, np.full(C, -(1 << 30)))
+        ch.process(case.iq)
+        with pytest.raises(_lib.MkidError) as e:
+            ch.trigger_phase(np.zeros((8, C), np.int16))
+        assert e.value.code == _lib.MKID_E_STATE
+        ch.reset()
+        ch.trigger_phase(np.zeros((8, C), np.int16))
+        with pytest.raises(_lib.MkidError) as e:
+            ch.process(case.iq)
+        assert e.value.code == _lib.MKID_E_STATE
+        ch.reset()
+        ch.process(case.iq)
+    finally:
+        ch.close()

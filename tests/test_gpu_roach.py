@@ -214,3 +214,42 @@ def test_lo_sweep_loop_calibration(gpu):
     phase, _ = roach.run(2048)
     tone_phase = np.angle(np.exp(1j * phase[64:, :len(freqs)]).mean(0))
     assert np.abs(tone_phase).max() < 0.05, tone_phase
+
+
+def test_longsnapshot_and_contsnapshot(gpu, tmp_path):
+    """ROACH_Pulses.py longsnapshot (433-551) and contsnapshot (557-762) through the shim on the
+    GPU: 2^19 qdr0 words = 2^20 device phase samples of one channel; the noise-FFT bins equal the
+    reference's saved ch_noifreqs_0.txt (fftfreq(10485)), the spectrum equals the loop-for-loop
+    restatement on the same qdr phase, and contsnapshot's device block-mean hits, windows and
+    pulse numbers equal the restated loop (failsafe included)."""
+    from oracle import replay as oreplay
+    C = 64
+    roach = FpgaClient(n_channels=C, noise_sigma=60.0, seed=5)
+    roach.progdev('pulse_trigger_2022_Jan_24_1322.bof')
+    freqs = [4.0e9 + 37e6 + 15625.0 * 3, 4.0e9 - 120e6]
+    rs = RoachSetup(roach, freqs, 4.0e9, n_channels=C)
+    rs.define_LUTs()
+    rs.toggleDAC()
+    rs.rotateLoopsReady()
+    rp = RoachPulses(roach, 2, None, n_channels=C)
+    ls = rp.longsnapshot(0, steps=1, save_dir=str(tmp_path))
+    assert len(ls['qdr_phase']) == 2 ** 20 and len(ls['phase']) == 2 * 1024
+    ref_freqs = np.loadtxt(os.path.join(GOLD, 'ch_noifreqs_0.txt'))
+    assert ls['noiseFFTFreqs'].shape == ref_freqs.shape == (10485,)
+    assert np.allclose(ls['noiseFFTFreqs'], ref_freqs, rtol=0, atol=1e-12)
+    f2, n2 = oreplay.noise_spectrum_loop(ls['qdr_phase'])
+    assert np.array_equal(f2, ls['noiseFFTFreqs'])
+    assert np.allclose(ls['noiseFFT'], n2, rtol=1e-12, atol=1e-9)
+    assert np.isfinite(ls['noiseFFT'][1:]).all()
+    assert np.allclose(np.loadtxt(str(tmp_path / 'ch_noifreqs_0.txt')), ref_freqs, atol=1e-12)
+    # noise only: a threshold of a few degrees fires on the noise tails
+    sd = float(np.std(ls['qdr_phase']))
+    thr = 3.5 * sd
+    for maxloops in (None, 200000):
+        cs = rp.contsnapshot(0, steps=1, phase_threshold=thr, averagelength_power=10, maxloops=maxloops)
+        qdr = cs['qdr_phase']
+        hits, pn, fin = oreplay.contsnapshot_loop(qdr, thr, 1024, maxloops or (1 << 40))
+        assert cs['hits'] == hits
+        assert cs['pulsenumber'] == pn
+        assert np.array_equal(np.asarray(cs['phase']), np.asarray(fin))
+        assert len(hits) > 3

@@ -27,7 +27,7 @@ def synth_raw(C, J, seed, pulse_rate=1.0 / 2000):
     return np.clip(np.rint(ph), -25736, 25736).astype(np.int16)
 
 
-def run_both(raw, chunks, env=None, monkeypatch=None):
+def run_both(raw, chunks, env=None, monkeypatch=None, max_events_per_ch=0):
     from mkids_sdr_amd.channelizer import Channelizer
     C = raw.shape[1]
     mf = codecs.fir_quantise(np.loadtxt(os.path.join(GOLD, 'fir', 'matched_30us.txt')))
@@ -36,7 +36,7 @@ def run_both(raw, chunks, env=None, monkeypatch=None):
     thr = np.array([codecs.threshold_from_phase(quiet[:, c])[0] for c in range(C)], np.int32)
     for k, v in (env or {}).items():
         monkeypatch.setenv(k, str(v))
-    ch = Channelizer(C, max_chunk=max(chunks) * 2 * C)
+    ch = Channelizer(C, max_chunk=max(chunks) * 2 * C, max_events_per_ch=max_events_per_ch)
     try:
         ch.set_fir(taps)
         ch.set_thresholds(thr)
@@ -76,6 +76,21 @@ def test_svf_segments_forced_fixup_streamed(gpu, monkeypatch):
     raw = synth_raw(C, J, 4)
     got, exp, reruns = run_both(raw, [70000, 90000], env={'MKID_SVF_WARMUP': 520},
                                 monkeypatch=monkeypatch)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    assert reruns > 50
+
+
+@pytest.mark.gpu
+def test_svf_forced_fixup_small_event_cap(gpu, monkeypatch):
+    """A per-channel event cap far below an SVF segment's packet capacity (the fix-up
+    scratch was sized from the cap and the EMA segment length): every segment is re-run into the
+    scratch, packets exact."""
+    C, J = 128, 160000
+    raw = synth_raw(C, J, 5, pulse_rate=1.0 / 20000)
+    got, exp, reruns = run_both(raw, [70000, 90000], env={'MKID_SVF_WARMUP': 520},
+                                monkeypatch=monkeypatch, max_events_per_ch=24)
+    assert max(len(e) for e in exp) > 0
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
     assert reruns > 50

@@ -67,9 +67,9 @@ def _noise_iq(S, seed):
 
 
 @pytest.mark.gpu
-def test_heights_config5_split(gpu):
+def test_heights_config5_fused(gpu):
     from mkids_sdr_amd.channelizer import Channelizer
-    C, S = 2048, 2 ** 20                       # config 5 geometry: N = 4096, split front end
+    C, S = 2048, 2 ** 20                       # config 5 geometry: N = 4096, fused k_front4
     ch = Channelizer(C, max_chunk=S)
     try:
         ch.set_fir(np.tile(np.arange(26, dtype=np.int16) * 40 - 500, (C, 1)))
@@ -126,7 +126,9 @@ def test_heights_streamed_fused_j0(gpu):
 def test_heights_history_across_calls(gpu):
     """Heights after every call of a stream: windows that start before a call's first row read
     the context's carried copy of the previous call's last rows, so every packet of the second
-    call whose window ends inside the stream equals the oracle on the concatenated phase."""
+    call whose window ends inside the stream equals the oracle on the concatenated phase. The
+    first call's packets whose windows ran past its last row come back NaN; passed again with the
+    second call (include/mkidgpu.h: deferral) they get their heights too."""
     import torch
     from mkids_sdr_amd.channelizer import Channelizer
     C, S, pre, nco = 1024, 2 ** 20, 20, 100
@@ -139,6 +141,7 @@ def test_heights_history_across_calls(gpu):
         ch.set_pulse_filter(coeff, pre=pre)
         x = torch.from_numpy(_noise_iq(2 * S, 66)).cuda()
         phases, evs, hs = [], [], []
+        deferred = np.zeros(0, np.uint64)
         for k in range(2):
             d_ph = torch.empty((J, C), dtype=torch.float32, device='cuda')
             d_ev = torch.empty(J * C, dtype=torch.int64, device='cuda')
@@ -146,12 +149,25 @@ def test_heights_history_across_calls(gpu):
             ch.process_device(x[k * S:(k + 1) * S], S, d_ph, d_ev, J * C, d_cnt)
             torch.cuda.synchronize()
             n = int(d_cnt[1].item())
-            d_h = torch.empty(max(n, 1), dtype=torch.float32, device='cuda')
-            ch.pulse_heights_device(d_ph, J, k * J, d_ev, n, d_h)
+            ev = np.concatenate([deferred, d_ev[:n].cpu().numpy().view(np.uint64)])
+            d_all = torch.from_numpy(ev.view(np.int64).copy()).cuda()
+            d_h = torch.empty(max(len(ev), 1), dtype=torch.float32, device='cuda')
             torch.cuda.synchronize()
+            ch.pulse_heights_device(d_ph, J, k * J, d_all, len(ev), d_h)
+            torch.cuda.synchronize()
+            h = d_h[:len(ev)].cpu().numpy()
             phases.append(d_ph.cpu().numpy())
-            evs.append(d_ev[:n].cpu().numpy().view(np.uint64))
-            hs.append(d_h[:n].cpu().numpy())
+            nd = len(deferred)
+            evs.append(ev[nd:])
+            hs.append(h[nd:])
+            if k == 0:
+                ts1 = (ev & np.uint64(oh.TS_MASK)).astype(np.int64)
+                tail = ts1 - pre + nco > J
+                assert tail.sum() > 5
+                assert np.array_equal(np.isnan(h), tail | (ts1 - pre < 0))
+                deferred = ev[tail]
+            else:
+                h_def, ev_def = h[:nd], ev[:nd]
     finally:
         ch.close()
     phase = np.concatenate(phases)
@@ -161,6 +177,8 @@ def test_heights_history_across_calls(gpu):
     assert early.sum() > 5
     assert np.all(np.isfinite(hs[1][early]))
     _check(phase, ev2, coeff.astype(np.float64), pre, 0, hs[1])
+    assert np.all(np.isfinite(h_def))
+    _check(phase, ev_def, coeff.astype(np.float64), pre, 0, h_def)
 
 
 @pytest.mark.gpu

@@ -315,3 +315,19 @@ def test_loopback_resonator_source():
         assert abs(got[k] - ref[k] * h) < 1e-9 * abs(ref[k])
         # the rest is the LUT's quantisation noise (each bin through its own transmission)
         assert np.abs(roach._adc_lut() - plain * h).max() < 0.01 * np.abs(plain).max()
+
+
+def test_noise_spectrum_matches_reference_loop():
+    """codecs.noise_spectrum (longsnapshot's phase-noise FFT, ROACH_Pulses.py:521-543) equals the
+    loop-for-loop restatement, and at the reference's 2^20-sample capture its bins are the
+    reference's saved ch_noifreqs_0.txt."""
+    from oracle import replay as oreplay
+    x = np.random.default_rng(3).normal(0, 5.0, 1 << 20) + 12.0
+    f, s = codecs.noise_spectrum(x)
+    f2, s2 = oreplay.noise_spectrum_loop(x)
+    assert np.array_equal(f, f2)
+    assert np.allclose(s, s2, rtol=1e-12, atol=1e-9)
+    ref = np.loadtxt(os.path.join(GOLD, 'ch_noifreqs_0.txt'))
+    assert np.allclose(f, ref, rtol=0, atol=1e-12)
+    raw = np.array([-25736, -1, 0, 1, 25736, 12345], np.int64)
+    assert np.array_equal(codecs.decode_qdr(raw.astype('>i2').tobytes()), raw)

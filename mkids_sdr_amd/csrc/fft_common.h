@@ -60,6 +60,23 @@ __device__ __forceinline__ float2 cmul_pk(float2 y, float2 t) {
     return float2_of(d);
 }
 
+// x + g * a with g one half of a uniform (SGPR) tap pair gp = (g_lo, g_hi): one v_pk_fma_f32
+// whose op_sel / op_sel_hi pick the same half of the pair for both lanes, so 13 pairs of
+// consecutive low-pass taps serve all 26 taps without duplicating any in SGPRs (the compiler
+// duplicates taps per pair and runs out of SGPRs, falling back to scalar v_fmac pairs)
+template <int HI>
+__device__ __forceinline__ float2 fma_tap(uint64_t gp, float2 a, float2 x) {
+    f2v d;
+    if constexpr (HI)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "=v"(d) : "s"(gp), "v"(f2v_of(a)), "v"(f2v_of(x)));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "=v"(d) : "s"(gp), "v"(f2v_of(a)), "v"(f2v_of(x)));
+    return float2_of(d);
+}
+__device__ __forceinline__ uint64_t tap_pair(float lo, float hi) {
+    return (uint64_t)__builtin_bit_cast(uint32_t, lo) | ((uint64_t)__builtin_bit_cast(uint32_t, hi) << 32);
+}
+
 __device__ __forceinline__ void dft2(float2& a, float2& b) {
     float2 t = a;
     a = cadd(t, b);

@@ -229,6 +229,10 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
         tl[q - 1] = make_float2((float)cs, (float)sn);
     }
     const int yoff = yswz(bin & 511);
+    // low-pass taps as 13 uniform pairs (g_{2m}, g_{2m+1}) for packed FMAs (fma_tap)
+    uint64_t gp[13];
+#pragma unroll
+    for (int m = 0; m < 13; ++m) gp[m] = tap_pair(a.taps.g[2 * m], a.taps.g[2 * m + 1]);
 
     const int64_t k_b = (int64_t)blockIdx.x * a.frames_per_block;
     int64_t k_e = k_b + a.frames_per_block;
@@ -249,7 +253,6 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
             ring_put<N>(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
         }
     }
-    uint4 pre = load4<N>(a, k_start + FPB, tid);
     __syncthreads();
 
     float2 acc[13];
@@ -284,6 +287,9 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
         ++it_;
         STAMP2(14);
 #endif
+        // this iteration's ring refill (written after the FFT barrier), loaded first: no ring
+        // load is outstanding in the select phase (vmcnt waits are in issue order)
+        const uint4 pre = load4<N>(a, k_b + kr + FPB, tid);
         float2 lov[FPB];
 #pragma unroll
         for (int f = 0; f < FPB; ++f) lov[f] = (a.lo + ((lrow + f) & (a.P - 1)) * C)[c];
@@ -346,7 +352,6 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
             int ws = rb + qh;
             ws -= ws >= RS ? RS : 0;
             ring_put<N>(ring + ws * M, qoff, pre);
-            pre = load4<N>(a, k_b + kr + 2 * FPB, tid);
             rb += FPB;
             rb -= rb >= RS ? RS : 0;
             lrow += FPB;
@@ -363,19 +368,13 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
             const float2 z = MKID_CMUL(X, lov[f]);
             if ((f & 1) == 0) {
 #pragma unroll
-                for (int m = 0; m < 13; ++m) {
-                    acc[m].x = fmaf(a.taps.g[2 * m + 1], z.x, acc[m].x);
-                    acc[m].y = fmaf(a.taps.g[2 * m + 1], z.y, acc[m].y);
-                }
+                for (int m = 0; m < 13; ++m) acc[m] = fma_tap<1>(gp[m], z, acc[m]);   // g_{2m+1}
             } else {
                 // output frame: the accumulate and the shift to the next output are one FMA per
                 // accumulator (acc[m] <- acc[m+1] + g_{2m+2} z), no register moves
-                const float2 y = make_float2(fmaf(a.taps.g[0], z.x, acc[0].x), fmaf(a.taps.g[0], z.y, acc[0].y));
+                const float2 y = fma_tap<0>(gp[0], z, acc[0]);                          // g_0
 #pragma unroll
-                for (int m = 0; m < 12; ++m) {
-                    acc[m].x = fmaf(a.taps.g[2 * m + 2], z.x, acc[m + 1].x);
-                    acc[m].y = fmaf(a.taps.g[2 * m + 2], z.y, acc[m + 1].y);
-                }
+                for (int m = 0; m < 12; ++m) acc[m] = fma_tap<0>(gp[m + 1], z, acc[m + 1]);  // g_{2m+2}
                 acc[12] = make_float2(0.f, 0.f);
                 if (kf > 0 && kf < nrun) {
                     const int jr = (kf - 1) >> 1;

@@ -26,6 +26,22 @@
 #define MKID_NT_STORES 1
 #endif
 
+#ifdef MKID_XP_STAMPS
+// timing-only build: lane 0 of every wave of workgroups 0-3 stamps s_memtime at 6 points of
+// iterations 8..15 into a.phase (tools/stamps4.py); the phase output of that build is garbage
+#define STAMP4(slot_)                                                                             \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        const uint64_t tm_ = __builtin_amdgcn_s_memtime();                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        if (blockIdx.x < 4 && it_ >= 8 && it_ < 16 && (threadIdx.x & 63) == 0)                   \
+            reinterpret_cast<uint64_t*>(a.phase)[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 +   \
+                                                  (it_ - 8)) * 8 + (slot_)] = tm_;                \
+    } while (0)
+#else
+#define STAMP4(slot_) ((void)0)
+#endif
+
 namespace mkid {
 
 namespace {
@@ -193,6 +209,11 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
         qc[q] = a.qc[c];
     }
 
+    // low-pass taps as 13 uniform pairs (g_{2m}, g_{2m+1}) for packed FMAs (fma_tap)
+    uint64_t gp[13];
+#pragma unroll
+    for (int m = 0; m < 13; ++m) gp[m] = tap_pair(a.taps.g[2 * m], a.taps.g[2 * m + 1]);
+
     const int64_t k_b = (int64_t)blockIdx.x * a.frames_per_block;
     int64_t k_e = k_b + a.frames_per_block;
     if (k_e > a.K) k_e = a.K;
@@ -212,8 +233,6 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
             ring_put8(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v0, v1);
         }
     }
-    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0;
-    load8(a, k_start + FPB, tid, pre0, pre1);
     __syncthreads();
 
     float2 acc[CPT][13];
@@ -232,7 +251,19 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
     const float2* t1 = tw1 + L;
     const float2* t2 = tw2 + la;
 
+#ifdef MKID_XP_STAMPS
+    int it_ = 0;
+#endif
     for (int kr = -kLpfHist; kr < nrun; kr += FPB) {
+#ifdef MKID_XP_STAMPS
+        ++it_;
+#endif
+        STAMP4(0);
+        // this iteration's ring refill (its oldest FPB hops, written after the FFT barrier):
+        // loaded here, so the 8 registers live only through the FFT phase and no ring load is
+        // outstanding in the select phase (vmcnt waits are in issue order)
+        uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0;
+        load8(a, k_b + kr + FPB, tid, pre0, pre1);
         // LO rows of the iteration's frames: scalar row base + 32-bit lane offsets (global_load
         // with an SGPR base). Loaded here (live across the FFT) with 512-thread workgroups; with
         // 1024 (2 channels per thread, 128 VGPRs) after the FFT, where the registers are free
@@ -298,18 +329,20 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
         }
+        STAMP4(1);
         __syncthreads();  // Y of both frames visible; every ring read of this iteration done
+        STAMP4(2);
         if constexpr (G::BT != 512) load_lo();
 
         {   // ring refill for the next iteration (its oldest FPB hops), prefetch one further
             int ws = rb + qh;
             ws -= ws >= RS ? RS : 0;
             ring_put8(ring + ws * M, qoff, pre0, pre1);
-            load8(a, k_b + kr + 2 * FPB, tid, pre0, pre1);
             rb += FPB;
             rb -= rb >= RS ? RS : 0;
             lrow += FPB;
         }
+        STAMP4(3);
 
         // ---- select (Horner in W_N^bin) + DDC + low-pass + phase, channels tid + 512 q ----
 #pragma unroll
@@ -337,23 +370,16 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
 #pragma unroll
                 for (int m = 0; m < 13; ++m)
 #pragma unroll
-                    for (int q = 0; q < CPT; ++q) {
-                        acc[q][m].x = fmaf(a.taps.g[2 * m + 1], z[q].x, acc[q][m].x);
-                        acc[q][m].y = fmaf(a.taps.g[2 * m + 1], z[q].y, acc[q][m].y);
-                    }
+                    for (int q = 0; q < CPT; ++q) acc[q][m] = fma_tap<1>(gp[m], z[q], acc[q][m]);   // g_{2m+1}
             } else {
                 // output frame: accumulate and shift to the next output in one FMA each
                 float2 y[CPT];
 #pragma unroll
-                for (int q = 0; q < CPT; ++q)
-                    y[q] = make_float2(fmaf(a.taps.g[0], z[q].x, acc[q][0].x), fmaf(a.taps.g[0], z[q].y, acc[q][0].y));
+                for (int q = 0; q < CPT; ++q) y[q] = fma_tap<0>(gp[0], z[q], acc[q][0]);             // g_0
 #pragma unroll
                 for (int m = 0; m < 12; ++m)
 #pragma unroll
-                    for (int q = 0; q < CPT; ++q) {
-                        acc[q][m].x = fmaf(a.taps.g[2 * m + 2], z[q].x, acc[q][m + 1].x);
-                        acc[q][m].y = fmaf(a.taps.g[2 * m + 2], z[q].y, acc[q][m + 1].y);
-                    }
+                    for (int q = 0; q < CPT; ++q) acc[q][m] = fma_tap<0>(gp[m + 1], z[q], acc[q][m + 1]);  // g_{2m+2}
 #pragma unroll
                 for (int q = 0; q < CPT; ++q) acc[q][12] = make_float2(0.f, 0.f);
                 if (kf > 0 && kf < nrun) {
@@ -371,7 +397,9 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
                         int qv = __float2int_rn(ph[q] * 8192.0f);
                         qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
 #if MKID_NT_STORES
+#ifndef MKID_XP_STAMPS
                         if (phase_run) __builtin_nontemporal_store(ph[q], phase_run + jr * C + c);
+#endif
                         __builtin_nontemporal_store((int16_t)qv, raw_run + jr * C + c);
 #else
                         if (phase_run) (phase_run + jr * C)[c] = ph[q];
@@ -385,7 +413,9 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
                 }
             }
         }
+        STAMP4(4);
         __syncthreads();  // select reads done before the next iteration's region writes
+        STAMP4(5);
     }
     if (a.ysum)
 #pragma unroll

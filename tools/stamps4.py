@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Phase timing of k_front4 (N = 4096) from in-kernel s_memtime stamps (a build with
+-DMKID_XP_STAMPS): lane 0 of each wave of workgroups 0-3 stamps 6 points of iterations 8..15.
+
+    bash tools/build_variant.sh f4_stamps -- -DMKID_XP_STAMPS
+    python tools/stamps4.py build/variants/f4_stamps.so
+Prints mean cycles per segment over waves and iterations. Timing only: the phase output of that
+build holds the stamps.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SEG = [('FFT phase (PFB, 3 x radix-8, T1/T2, Y write)', 0, 1), ('barrier 1 wait', 1, 2),
+       ('LO load issue + ring refill', 2, 3), ('select + DDC + low-pass + output', 3, 4),
+       ('barrier 2 wait', 4, 5), ('loop back', 5, 'next0')]
+
+
+SEG2 = [('FFT phase (PFB, 3 x radix-8, T1/T2, Y write)', 14, 0), ('barrier 1 wait', 0, 1),
+        ('refill + select + DDC + low-pass + output', 1, 2), ('barrier 2 wait', 2, 3),
+        ('loop back', 3, 'next14')]
+
+
+def main():
+    import torch
+    from mkids_sdr_amd.channelizer import Channelizer
+    lib = os.path.abspath(sys.argv[1])
+    C = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+    N = 2 * C
+    S = 1 << 28
+    dev = torch.device('cuda', 0)
+    ch = Channelizer(C, max_chunk=S, lib_path=lib)
+    x = torch.randint(-2000, 2000, (2 * S,), dtype=torch.int16, device=dev)
+    phase = torch.zeros(S // N * C, dtype=torch.float32, device=dev)
+    ev = torch.empty(1 << 20, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    ch.set_thresholds(np.full(C, -(1 << 30), np.int32))
+    for _ in range(3):
+        phase.zero_()
+        ch.process_device(x, S, phase, ev, ev.numel(), cnt)
+        torch.cuda.synchronize()
+    if C == 2048:   # k_front4: 8 stamps per (wave, iteration)
+        st = phase[:4 * 16 * 8 * 8 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 8)
+        seg, top = SEG, 0
+    else:           # k_front2: 16 stamp slots per (wave, iteration), loop top in slot 14
+        st = phase[:4 * 16 * 8 * 16 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 16)
+        seg, top = SEG2, 14
+    out = {}
+    tot = 0.0
+    for name, a, b in seg:
+        d = st[:, :, 1:, top] - st[:, :, :-1, a] if str(b).startswith('next') else st[:, :, :, b] - st[:, :, :, a]
+        m = float(np.mean(d))
+        tot += m
+        out[name] = dict(mean=round(m), min=int(d.min()), max=int(d.max()))
+        print('%-46s %8.0f cycles  (min %6d max %6d)' % (name, m, int(d.min()), int(d.max())))
+    it = st[:, :, 1:, top] - st[:, :, :-1, top]
+    print('%-46s %8.0f cycles  (sum of segments %.0f)' % ('iteration', float(np.mean(it)), tot))
+    out['iteration'] = round(float(np.mean(it)))
+    print(json.dumps(out))
+    ch.close()
+
+
+if __name__ == '__main__':
+    main()

@@ -407,6 +407,312 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
     if (a.ysum) ysum_add(a.ysum, c, ys.x, ys.y);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// k_front3 (N = 2048, config 3): the k_front2 arithmetic with WAVE SPECIALISATION. In k_front2
+// every wave runs the FFT phase, then every wave runs the select phase, with a workgroup barrier
+// between them: when all four waves of a SIMD wait on LDS (ring reads, the select's bin-indexed
+// reads) or on a barrier, the SIMD idles (stamps: the FFT phase of the last wave of a SIMD ends
+// ~2.4k cycles after the first, VALU busy ~70 %). Here waves 0-7 only transform (2 frames per
+// iteration, one 512-point sub-FFT each) and waves 8-15 only select / mix / low-pass / phase
+// (two channels per thread), one iteration behind, on a double-buffered Y: each SIMD holds two
+// FFT and two select waves whose LDS waits and VALU bursts interleave, one barrier per iteration.
+//   ring  RS = 2T - 1 + 2F hops: iteration t reads hops k-7 .. k+1 (frames k, k+1) while its
+//         FFT waves write hops k+2, k+3 (prefetched at the loop top) over hops k-9, k-8
+//   Y     [2][F][NW][576] float2, iteration t writes buffer t & 1, its select reads (t - 1) & 1
+// Registers: the FFT path holds the PFB taps and the 512-point sub-FFT, the select path two
+// channels' low-pass state; branches are wave-uniform, so the two live sets do not add up.
+template <int N>
+struct G3 {
+    static constexpr int NW = N / 512;
+    static constexpr int FW = 8;                       // transform waves
+    static constexpr int F = FW / NW;                  // frames per iteration
+    static constexpr int BT = 1024;
+    static constexpr int SPT = BT - FW * 64;           // select threads
+    static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
+    static constexpr int CPT = C / SPT;                // channels per select thread
+    static constexpr int RS = 2 * T - 1 + 2 * F;       // ring slots (hops)
+    static constexpr int REG = 576;
+    static constexpr int FB = NW * REG;
+    static constexpr size_t off_fbuf = (size_t)RS * M * 4;
+    static constexpr size_t off_tw1 = off_fbuf + (size_t)2 * F * FB * 8;
+    static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;
+    static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
+    static_assert(N == 2048 && F == 2 && CPT == 2 && F * M == FW * 64 * 4, "k_front3 geometry");
+    static_assert(lds_bytes <= 160 * 1024, "LDS");
+};
+
+#ifdef MKID_XP_STAMPS
+#define STAMP3(slot_)                                                                             \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        const uint64_t tm_ = __builtin_amdgcn_s_memtime();                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        if (blockIdx.x < 4 && t >= 8 && t < 16 && (threadIdx.x & 63) == 0)                        \
+            reinterpret_cast<uint64_t*>(a.phase)[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 +   \
+                                                  (t - 8)) * 16 + (slot_)] = tm_;                 \
+    } while (0)
+#else
+#define STAMP3(slot_) ((void)0)
+#endif
+
+template <int N>
+__global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
+    using G = G3<N>;
+    constexpr int NW = G::NW, M = G::M, C = G::C, T = G::T, RS = G::RS, F = G::F, CPT = G::CPT;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
+    float2* fbuf = reinterpret_cast<float2*>(smem + G::off_fbuf);
+    float2* tw1 = reinterpret_cast<float2*>(smem + G::off_tw1);
+    float2* tw2 = reinterpret_cast<float2*>(smem + G::off_tw2);
+
+    const int tid = threadIdx.x;
+    const int L = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool xform = wave < G::FW;
+
+    for (int i = tid; i < 7 * 64; i += G::BT) {
+        const int k = i / 64 + 1, l = i % 64;
+        double sn, cs;
+        sincospi(-2.0 * (double)(l * k) / 512.0, &sn, &cs);
+        tw1[i] = make_float2((float)cs, (float)sn);
+    }
+    for (int i = tid; i < 7 * 8; i += G::BT) {
+        const int k = i / 8 + 1, l = i % 8;
+        double sn, cs;
+        sincospi(-2.0 * (double)(l * k) / 64.0, &sn, &cs);
+        tw2[i] = make_float2((float)cs, (float)sn);
+    }
+
+    const int64_t k_b = (int64_t)blockIdx.x * a.frames_per_block;
+    int64_t k_e = k_b + a.frames_per_block;
+    if (k_e > a.K) k_e = a.K;
+    if (k_b >= k_e) return;
+    const int64_t k_start = k_b - kLpfHist;
+    const int nrun = (int)(k_e - k_b);
+    const int nit = (nrun + kLpfHist + F - 1) / F;    // iterations of F frames from k_start
+
+#ifndef MKID_F3_PRIO_X
+#define MKID_F3_PRIO_X 0
+#endif
+#ifndef MKID_F3_PRIO_S
+#define MKID_F3_PRIO_S 0
+#endif
+    if (xform) {
+        // ---------------- transform waves: PFB + 512-point sub-FFT of (frame slot, w) ----------
+        if (MKID_F3_PRIO_X) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_X);
+        const int slot = wave / NW, w = wave % NW;
+        const int qh = (tid * 4) / M, qoff = (tid * 4) % M;   // this thread's ring write
+        {   // prologue: hops k_start-2T+1 .. k_start+F-1
+            const int64_t h0 = k_start - 2 * T + 1;
+            for (int g = 0; g < 2 * T - 1 + F; g += 2) {
+                const int64_t hop = h0 + g + qh;
+                if (hop > h0 + 2 * T - 2 + F) continue;
+                const uint4 v = load4<N>(a, h0 + g, tid);
+                ring_put<N>(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
+            }
+        }
+        uint2 tq[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
+        const int la = L & 7, kl = L >> 3;
+        const float2* t1 = tw1 + L;
+        const float2* t2 = tw2 + la;
+        int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);   // slot of hop k - 2T + 1
+        __syncthreads();
+        for (int t = 0; t <= nit; ++t) {
+            STAMP3(0);
+            if (t < nit) {
+                const int kr = -kLpfHist + F * t;
+                // the hops iteration t + 1 adds: loaded now, written after this wave's PFB
+                const uint4 pre = load4<N>(a, k_b + kr + F, tid);
+                float2* reg = fbuf + ((t & 1) * F + slot) * G::FB + w * G::REG;
+                int sb = rb + slot;
+                sb -= sb >= RS ? RS : 0;
+                float2 v[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int hi = r >> 2;
+                    const int pos = w * (M / NW) + 64 * (r & 3) + L;
+                    uint32_t x4[T];
+#pragma unroll
+                    for (int tau = 0; tau < T; ++tau) {
+                        int sl = sb + 2 * tau + hi;
+                        sl -= sl >= RS ? RS : 0;
+                        x4[tau] = ring[sl * M + pos];
+                    }
+                    const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
+                    const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
+                    const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);
+                    const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x07060302u);
+                    int32_t ai = dot2_first(tq[r].x, i01);
+                    ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
+                    int32_t aq = dot2_first(tq[r].x, q01);
+                    aq = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(q23), aq, false);
+                    v[r] = make_float2((float)ai, (float)aq);
+                }
+                dft<8>(v);
+#pragma unroll
+                for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t1[64 * (k - 1)]);
+                t1_transpose(v);
+                dft<8>(v);
+#pragma unroll
+                for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t2[8 * (k - 1)]);
+                float2* t2w = reg + 72 * kl + la;
+                const float2* t2r = reg + 72 * kl + 9 * la;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) t2w[9 * r] = v[r];
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] = t2r[r];
+                dft<8>(v);
+                __builtin_amdgcn_wave_barrier();
+                float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
+#pragma unroll
+                for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
+                // ring refill: hops k+F .. k+2F-1 over hops k-2T-1 .. (no reader this iteration)
+                int ws = rb + 2 * T - 1 + F + qh;
+                ws -= ws >= RS ? RS : 0;
+                ws -= ws >= RS ? RS : 0;
+                ring_put<N>(ring + ws * M, qoff, pre);
+                rb += F;
+                rb -= rb >= RS ? RS : 0;
+            }
+            STAMP3(1);
+            __syncthreads();
+            STAMP3(2);
+        }
+    } else {
+        // ---------------- select waves: channels st + SPT q, one iteration behind ---------------
+        if (MKID_F3_PRIO_S) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_S);
+        const int st = tid - G::FW * 64;
+        float2 tl[CPT][NW - 1];
+        int yoff[CPT];
+        float ic[CPT], qc[CPT];
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const int c = st + G::SPT * q;
+            const int32_t bin = a.bins[c];
+#pragma unroll
+            for (int u = 1; u < NW; ++u) {
+                double sn, cs;
+                sincospi(-2.0 * (double)((u * bin) % N) / N, &sn, &cs);
+                tl[q][u - 1] = make_float2((float)cs, (float)sn);
+            }
+            yoff[q] = yswz(bin & 511);
+            ic[q] = a.ic[c];
+            qc[q] = a.qc[c];
+        }
+        uint64_t gp[13];
+#pragma unroll
+        for (int m = 0; m < 13; ++m) gp[m] = tap_pair(a.taps.g[2 * m], a.taps.g[2 * m + 1]);
+        float2 acc[CPT][13];
+#pragma unroll
+        for (int q = 0; q < CPT; ++q)
+#pragma unroll
+            for (int m = 0; m < 13; ++m) acc[q][m] = make_float2(0.f, 0.f);
+        float2 ys[CPT];
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) ys[q] = make_float2(0.f, 0.f);
+        int16_t* const raw_run = a.raw + (k_b >> 1) * C;
+        float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
+        int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
+        __syncthreads();
+        for (int t = 0; t <= nit; ++t) {
+            STAMP3(3);
+            if (t > 0) {
+                const int kr = -kLpfHist + F * (t - 1);
+                float2 lov[F][CPT];
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    const float2* row = a.lo + ((lrow + f) & (a.P - 1)) * C;
+#pragma unroll
+                    for (int q = 0; q < CPT; ++q) lov[f][q] = row[st + G::SPT * q];
+                }
+                lrow += F;
+#pragma unroll
+                for (int f = 0; f < F; ++f) {
+                    const int kf = kr + f;
+                    const float2* yf = fbuf + (((t - 1) & 1) * F + f) * G::FB;
+                    float2 z[CPT];
+#pragma unroll
+                    for (int q = 0; q < CPT; ++q) {
+                        float2 X = yf[yoff[q]];
+#pragma unroll
+                        for (int u = 1; u < NW; ++u) X = cmac(X, tl[q][u - 1], yf[yoff[q] + u * G::REG]);
+                        z[q] = MKID_CMUL(X, lov[f][q]);
+                    }
+                    if ((f & 1) == 0) {
+#pragma unroll
+                        for (int m = 0; m < 13; ++m)
+#pragma unroll
+                            for (int q = 0; q < CPT; ++q) acc[q][m] = fma_tap<1>(gp[m], z[q], acc[q][m]);
+                    } else {
+                        float2 y[CPT];
+#pragma unroll
+                        for (int q = 0; q < CPT; ++q) y[q] = fma_tap<0>(gp[0], z[q], acc[q][0]);
+#pragma unroll
+                        for (int m = 0; m < 12; ++m)
+#pragma unroll
+                            for (int q = 0; q < CPT; ++q) acc[q][m] = fma_tap<0>(gp[m + 1], z[q], acc[q][m + 1]);
+#pragma unroll
+                        for (int q = 0; q < CPT; ++q) acc[q][12] = make_float2(0.f, 0.f);
+                        if (kf > 0 && kf < nrun) {
+                            const int jr = (kf - 1) >> 1;
+#pragma unroll
+                            for (int q = 0; q < CPT; ++q) {
+                                const int c = st + G::SPT * q;
+                                ys[q].x += y[q].x;
+                                ys[q].y += y[q].y;
+                                const float ph = phase_atan2(y[q].y - qc[q], y[q].x - ic[q]);
+                                int qv = __float2int_rn(ph * 8192.0f);
+                                qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
+#if MKID_NT_STORES
+#ifndef MKID_XP_STAMPS
+                                if (phase_run) __builtin_nontemporal_store(ph, phase_run + jr * C + c);
+#endif
+                                __builtin_nontemporal_store((int16_t)qv, raw_run + jr * C + c);
+#else
+                                if (phase_run) (phase_run + jr * C)[c] = ph;
+                                (raw_run + jr * C)[c] = (int16_t)qv;
+#endif
+                                if (c == a.iq_ch && a.iqtap) {
+                                    a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y[q].x);
+                                    a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y[q].y);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            STAMP3(4);
+            __syncthreads();
+            STAMP3(5);
+        }
+        if (a.ysum)
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) ysum_add(a.ysum, st + G::SPT * q, ys[q].x, ys[q].y);
+    }
+}
+
+template <int N>
+static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
+    using G = G3<N>;
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front3<N>, (int)G::lds_bytes);
+    if (e != hipSuccess) return e;
+    FrontArgs a = a0;
+    if (a.K <= 0) return hipSuccess;
+    const int64_t ncu = a.ncu > 0 ? a.ncu : 256;
+    int64_t fpb = a.K / ncu;                     // one run per CU, as k_front2
+    fpb = fpb < 64 ? 64 : (fpb > 4096 ? 4096 : fpb);
+    fpb = (fpb + G::F - 1) / G::F * G::F;
+    a.frames_per_block = fpb;
+    const int64_t blocks = (a.K + fpb - 1) / fpb;
+    hipLaunchKernelGGL(k_front3<N>, dim3((unsigned)blocks), dim3(G::BT), G::lds_bytes, s, a);
+    return hipGetLastError();
+}
+
 bool front2_supported(int N) { return N == 512 || N == 1024 || N == 2048; }
 
 template <int N>
@@ -435,6 +741,7 @@ static hipError_t launch_front2_n(const FrontArgs& a0, hipStream_t s) {
 }
 
 hipError_t launch_front2(int N, const FrontArgs& a, hipStream_t s) {
+    if (N == 2048 && a.variant == 3) return launch_front3_n<2048>(a, s);
     switch (N) {
         case 512: return launch_front2_n<512>(a, s);
         case 1024: return launch_front2_n<1024>(a, s);

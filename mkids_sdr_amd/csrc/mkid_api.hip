@@ -116,6 +116,7 @@ struct mkid_ctx {
     int64_t last_raw_row = 0;       // first row of the last sub-chunk's raw phase in d_raw
     bool fused = false;  // K1-K6 in one kernel (k_front / k_front2 / k_front4: no z buffers, no stream B work)
     bool front_v2 = false;  // fused front end is k_front2 (N = 512..2048; MKID_FRONT_V1=1 forces v1)
+    int front_variant = 3;  // N = 2048: 3 = wave-specialised k_front3 (MKID_FRONT_V3=0: k_front2)
     int64_t H = 0;       // ADC history samples carried between calls
     // workspace
     float2* d_zb[2] = {nullptr, nullptr};
@@ -355,6 +356,8 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     {
         const char* v1 = getenv("MKID_FRONT_V1");
         c->front_v2 = c->fused && front2_supported(N) && !(v1 && atoi(v1) != 0);
+        const char* v3 = getenv("MKID_FRONT_V3");
+        c->front_variant = (v3 && atoi(v3) == 0) ? 2 : 3;
     }
     // split front end: a large call is cut into 4 sub-chunks so the channeliser (stream A) of
     // sub-chunk i+1 overlaps the low-pass/trigger (stream B) of sub-chunk i
@@ -834,6 +837,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.taps = c->lpf;
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
+        fa.variant = c->front_variant;
         tstart(c, MKID_K_FRONT, &kt, A);
         HIPCHK(c, front4_supported(N) ? launch_front4(fa, A)
                                       : (c->front_v2 ? launch_front2(N, fa, A) : launch_front(N, fa, A)));

@@ -97,6 +97,7 @@ struct FrontArgs {
     LpfTaps taps;
     int16_t* iqtap;         // [K/2][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
     int32_t iq_ch;
+    int32_t variant;        // N = 2048: 3 = wave-specialised k_front3, else k_front2
 };
 
 struct TrigSpecArgs {

@@ -26,6 +26,12 @@ SEG2 = [('FFT phase (PFB, 3 x radix-8, T1/T2, Y write)', 14, 0), ('barrier 1 wai
         ('loop back', 3, 'next14')]
 
 
+SEG3 = [('transform waves: PFB + sub-FFT + ring write', 0, 1), ('transform waves: barrier wait', 1, 2),
+        ('transform waves: loop back', 2, 'next0'),
+        ('select waves: LO + select + DDC + low-pass + output', 3, 4), ('select waves: barrier wait', 4, 5),
+        ('select waves: loop back', 5, 'next3')]
+
+
 def main():
     import torch
     from mkids_sdr_amd.channelizer import Channelizer
@@ -44,6 +50,18 @@ def main():
         phase.zero_()
         ch.process_device(x, S, phase, ev, ev.numel(), cnt)
         torch.cuda.synchronize()
+    if len(sys.argv) > 3 and sys.argv[3] == 'v3':   # k_front3: waves 0-7 transform, 8-15 select
+        st = phase[:4 * 16 * 8 * 16 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 16)
+        for name, a_, b_ in SEG3:
+            w = slice(0, 8) if a_ < 3 else slice(8, 16)
+            top = 0 if a_ < 3 else 3
+            x = st[:, w]
+            d = x[:, :, 1:, top] - x[:, :, :-1, a_] if str(b_).startswith('next') else x[:, :, :, b_] - x[:, :, :, a_]
+            print('%-52s %8.0f cycles  (min %6d max %6d)' % (name, float(np.mean(d)), int(d.min()), int(d.max())))
+        it = st[:, :8, 1:, 0] - st[:, :8, :-1, 0]
+        print('%-52s %8.0f cycles' % ('iteration (2 frames)', float(np.mean(it))))
+        ch.close()
+        return
     if C == 2048:   # k_front4: 8 stamps per (wave, iteration)
         st = phase[:4 * 16 * 8 * 8 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 8)
         seg, top = SEG, 0

@@ -63,9 +63,32 @@ def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32, front='auto'):
     return np.concatenate(phases), np.concatenate(evs), (mi, mq)
 
 
+_CASES, _ORACLE = {}, {}
+
+
+def cached_case(C, S, seed, pulses_per_ch):
+    """make_case + quiet thresholds, shared by the parametrisations that differ only in the
+    front end (the host-side case and oracle dominate the suite's time at 1024/2048 channels)."""
+    key = (C, S, seed, pulses_per_ch)
+    if key not in _CASES:
+        while len(_CASES) >= 3:                 # keep the last few cases (tens of MB each)
+            old = _CASES.pop(next(iter(_CASES)))
+            _ORACLE.pop(id(old[0]), None)
+        _CASES[key] = (signals.make_case(C, S, seed=seed, pulses_per_ch=pulses_per_ch),
+                       quiet_thresholds(C, min(S, 2 * C * 2048), seed))
+    return _CASES[key]
+
+
+def oracle_of(case):
+    if id(case) not in _ORACLE:
+        if not any(c[0] is case for c in _CASES.values()):
+            return signals.oracle_chain(case).process(case.iq)   # uncached case
+        _ORACLE[id(case)] = (case, signals.oracle_chain(case).process(case.iq))
+    return _ORACLE[id(case)][1]
+
+
 def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=True, front='auto'):
-    o = signals.oracle_chain(case)
-    r = o.process(case.iq)
+    r = oracle_of(case)
     tr = otrig.Trigger(case.C, case.fir12, thr, mode=mode, dead=dead)
     ev_o, n_o, _ = tr.run(r['raw'])
     ph_g, ev_g, _ = run_gpu(case, thr, splits, mode, max_chunk, dead, front)
@@ -121,12 +144,20 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     (2048, 2 ** 20, None, 6, 'split'),
 ])
 def test_chain_parity(gpu, C, S, splits, seed, front):
-    """Full chain vs the oracle. 'auto' runs the fused front end (k_front2 for N = 512..2048,
-    k_front4 for N = 4096, k_front for N = 128); 'split' runs k_channelize + k_lpf_phase with z
-    staged in HBM."""
-    case = signals.make_case(C, S, seed=seed, pulses_per_ch=max(1.0, S / (2 * C) / 400))
-    thr = quiet_thresholds(C, min(S, 2 * C * 2048), seed)
+    """Full chain vs the oracle. 'auto' runs the fused front end (k_front3 for N = 2048, k_front2
+    for N = 512/1024, k_front4 for N = 4096, k_front for N = 128); 'split' runs k_channelize +
+    k_lpf_phase with z staged in HBM."""
+    case, thr = cached_case(C, S, seed, max(1.0, S / (2 * C) / 400))
     compare(case, thr, splits or [0, S], front=front)
+
+
+def test_chain_parity_front2_at_2048(gpu, monkeypatch):
+    """The non-specialised k_front2 at N = 2048 (MKID_FRONT_V3=0; the default there is k_front3)
+    on config 3's parity case."""
+    monkeypatch.setenv('MKID_FRONT_V3', '0')
+    C, S = 1024, 2 ** 20
+    case, thr = cached_case(C, S, 5, max(1.0, S / (2 * C) / 400))
+    compare(case, thr, [0, 2 ** 19, S])
 
 
 @pytest.mark.parametrize('mode', [0, 1, 2])
@@ -272,8 +303,7 @@ def test_iq_snapshot_tap_matches_oracle(gpu, front):
     (64, 2 ** 16, None, 31, 1, False),
     (256, 2 ** 18, [0, 2 ** 17 + 512, 2 ** 18], 32, 1, True),
     (256, 2 ** 18, None, 33, 0, False),
-    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 34, 1, False),      # k_front2, N = 2048
-    (2048, 2 ** 20, [0, 2 ** 19 + 4096, 2 ** 20], 35, 1, True),  # k_front4, N = 4096
+    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 34, 1, True),       # fused N = 2048, deleted channels
 ])
 def test_fused_two_stream_pipeline(gpu, monkeypatch, C, S, splits, seed, mode, deleted):
     """process_fused's pipeline (front end of sub-chunk i+1 on stream A beside the lean trigger of

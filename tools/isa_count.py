@@ -63,18 +63,26 @@ def main():
         if pat not in name:
             continue
         labels = {}
-        best = None
+        spans = []
         for i, ln in enumerate(body):
             m = re.match(r'^(\.LBB\d+_\d+):', ln)
             if m:
                 labels[m.group(1)] = i
             m = re.search(r'\ts_cbranch_\w+\s+(\.LBB\d+_\d+)', ln) or re.search(r'\ts_branch\s+(\.LBB\d+_\d+)', ln)
             if m and m.group(1) in labels and labels[m.group(1)] < i:
-                span = (labels[m.group(1)], i)
-                if best is None or span[1] - span[0] > best[1] - best[0]:
-                    best = span
-        if best is None:
-            continue
+                spans.append((labels[m.group(1)], i))
+        # outermost loops, largest first (k_front3 has one per wave role)
+        spans.sort(key=lambda sp: sp[0] - sp[1])
+        outer = []
+        for sp in spans:
+            if not any(o[0] <= sp[0] and sp[1] <= o[1] for o in outer):
+                outer.append(sp)
+        for best in outer[:int(sys.argv[3]) if len(sys.argv) > 3 else 1]:
+            report(name, body, best)
+
+
+def report(name, body, best):
+    if True:
         cnt = Counter()
         for ln in body[best[0]:best[1] + 1]:
             s = ln.strip()

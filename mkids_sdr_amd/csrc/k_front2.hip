@@ -57,6 +57,9 @@
 #ifndef MKID_CMUL
 #define MKID_CMUL cmul_pk
 #endif
+#ifndef MKID_F2_T1LDS
+#define MKID_F2_T1LDS 1
+#endif
 // PFB tap quads in VGPRs (16 per lane; -1.1 % k_front2 same-box, profiles/r02_v11_kbench_f2_tapreg.json)
 #ifndef MKID_F2_TAPREG
 #define MKID_F2_TAPREG 1
@@ -138,7 +141,7 @@ __device__ __forceinline__ float upd_ror8(float old, float src) {
                                                                  BANKS, false));
 }
 
-__device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
+[[maybe_unused]] __device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
     // register bit 0 <-> lane bit 3: lanes 8-15 of every row (banks 2, 3) take the partner
     // register of lane ^ 8; lanes 0-7 (banks 0, 1) the other way round (row_ror:8 = lane ^ 8)
 #pragma unroll
@@ -174,6 +177,22 @@ __device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
 }
 
 __device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
+
+// T1 through the wave's own LDS region instead of DPP/permlane moves: element (lane 8 kl + la,
+// register r) goes to (lane 8 r + la, register kl). Lane L writes register r at 72 r + L; lane L'
+// reads register r' at 72 (L' >> 3) + 8 r' + (L' & 7). Both patterns are bank-conflict-free for
+// ds_*_b64 (writes: 32 consecutive entries; reads: entries 8 (r + r') + la mod 32 distinct over a
+// lane group, r = L' >> 3 < 4 there), every offset an immediate. 8 writes + 8 reads replace 32
+// VALU cross-lane moves (the transform waves are VALU-issue-bound).
+__device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) reg[72 * r + L] = v[r];
+    __builtin_amdgcn_wave_barrier();
+    const float2* rd = reg + 72 * (L >> 3) + (L & 7);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = rd[8 * r];
+    __builtin_amdgcn_wave_barrier();
+}
 
 }  // namespace
 
@@ -331,8 +350,12 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
         dft<8>(v);
 #pragma unroll
         for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t1[64 * (k - 1)]);
-        // ---- T1 (VALU cross-lane) + stage 2 + twiddle W_64^{la k} ----
+        // ---- T1 (through the wave's own LDS region, or VALU cross-lane) + stage 2 + twiddle ----
+#if MKID_F2_T1LDS
+        t1_lds(v, reg, L);
+#else
         t1_transpose(v);
+#endif
         dft<8>(v);
 #pragma unroll
         for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t2[8 * (k - 1)]);
@@ -422,6 +445,9 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
 //   Y     [2][F][NW][576] float2, iteration t writes buffer t & 1, its select reads (t - 1) & 1
 // Registers: the FFT path holds the PFB taps and the 512-point sub-FFT, the select path two
 // channels' low-pass state; branches are wave-uniform, so the two live sets do not add up.
+#ifndef MKID_F3_T1LDS
+#define MKID_F3_T1LDS 1
+#endif
 template <int N>
 struct G3 {
     static constexpr int NW = N / 512;
@@ -554,7 +580,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 dft<8>(v);
 #pragma unroll
                 for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t1[64 * (k - 1)]);
+#if MKID_F3_T1LDS
+                t1_lds(v, reg, L);
+#else
                 t1_transpose(v);
+#endif
                 dft<8>(v);
 #pragma unroll
                 for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t2[8 * (k - 1)]);

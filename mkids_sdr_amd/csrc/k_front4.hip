@@ -123,7 +123,7 @@ __device__ __forceinline__ float upd_ror8(float old, float src) {
 }
 
 // register bits <-> lane bits 3-5 (k_front2.hip t1_transpose)
-__device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
+[[maybe_unused]] __device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
 #pragma unroll
     for (int r0 = 0; r0 < 8; r0 += 2) {
         const float2 a0 = v[r0], a1 = v[r0 + 1];
@@ -155,6 +155,21 @@ __device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
 }
 
 __device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
+
+// T1 through the wave's own LDS region (k_front2.hip t1_lds): 8 + 8 conflict-free ds_*_b64
+// instead of 32 VALU cross-lane moves
+__device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) reg[72 * r + L] = v[r];
+    __builtin_amdgcn_wave_barrier();
+    const float2* rd = reg + 72 * (L >> 3) + (L & 7);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = rd[8 * r];
+    __builtin_amdgcn_wave_barrier();
+}
+#ifndef MKID_F4_T1LDS
+#define MKID_F4_T1LDS 1
+#endif
 
 }  // namespace
 
@@ -312,7 +327,11 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
             dft<8>(v);
 #pragma unroll
             for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], t1[64 * (k - 1)]);
+#if MKID_F4_T1LDS
+            t1_lds(v, reg, L);
+#else
             t1_transpose(v);
+#endif
             dft<8>(v);
 #pragma unroll
             for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], t2[8 * (k - 1)]);

@@ -212,6 +212,9 @@ def main():
                     help='0: every usable CPU (sched_getaffinity), capped at the cgroup CPU quota')
     ap.add_argument('--all-core-samples', type=int, required=True)
     ap.add_argument('--witness', default=None, help='.npz device outputs for the one-core sample')
+    ap.add_argument('--curve', default=None,
+                    help='comma-separated worker counts: time only the chunk-parallel leg at each (the '
+                         'cgroup cap is not applied), e.g. 4,8,16,32,64,256, and print one JSON line')
     a = ap.parse_args()
     import numpy as np
     cfg = _load_cfg(a.cfg)
@@ -221,6 +224,25 @@ def main():
     quota = cpu_quota_cores()
     out = dict(cpu_model=cpu_model(), os_cpu_count=os.cpu_count(), sched_affinity=len(aff),
                cpu_quota_cores=quota)
+    if a.curve:
+        import multiprocessing as mp
+        prefix = (16 + 520) * N
+        pts = []
+        for W in [int(x) for x in a.curve.split(',')]:
+            W = max(1, min(W, len(aff)))
+            n = a.all_core_samples - a.all_core_samples % (N * W)
+            per = n // W
+            blk = max(N, min(1 << 22, per) // N * N)
+            jobs = [(aff[i], a.input, a.cfg, i * per, (i + 1) * per, prefix, blk) for i in range(W)]
+            t0 = time.perf_counter()
+            with mp.get_context('fork').Pool(W) as pool:
+                res = pool.map(run_chunk, jobs)
+            wall = time.perf_counter() - t0
+            pts.append(dict(workers=W, value=round(sum(r[0] for r in res) / wall / 1e6, 3), wall_s=round(wall, 2),
+                            samples=int(sum(r[0] for r in res))))
+        out['curve'] = pts
+        print(json.dumps(out), flush=True)
+        return
     # >= (2T-1+24) hops of ADC history + 520 trigger warm-up rows (the EMA baseline's merge
     # horizon). The SVF baseline needs ~10^5 rows to merge exactly; its chunks use
     # the same prefix, so their first rows' packets are approximate (a timing baseline only).

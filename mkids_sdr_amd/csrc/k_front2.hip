@@ -178,6 +178,21 @@ __device__ __forceinline__ float upd_ror8(float old, float src) {
 
 __device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
 
+// k_front3 ring plane layout (N = 2048, NW = 4, Q = 256 samples per plane): plane index
+// i = 64 j + l (j = 0..3) is stored at 128 (j >> 1) + 2 l + (j & 1), so the PFB's points j and
+// j + 1 of a lane are one ds_read_b64 (16 reads of 8 B per sub-FFT instead of 32 of 4 B;
+// conflict-free: 32 lanes x 2 dwords). The refill's ds_write_b32 become 2-way bank conflicts,
+// which cost no extra cycles for ds_write_b32 (MI355X_MICROARCH.md §LDS).
+__device__ __forceinline__ int ring3_idx(int i) { return 128 * (i >> 7) + 2 * (i & 63) + ((i >> 6) & 1); }
+__device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
+    constexpr int Q = 256;
+    const int a = ring3_idx(qoff / 4);
+    hop[a] = v.x;
+    hop[Q + a] = v.y;
+    hop[2 * Q + a] = v.z;
+    hop[3 * Q + a] = v.w;
+}
+
 // T1 through the wave's own LDS region instead of DPP/permlane moves: element (lane 8 kl + la,
 // register r) goes to (lane 8 r + la, register kl). Lane L writes register r at 72 r + L; lane L'
 // reads register r' at 72 (L' >> 3) + 8 r' + (L' & 7). Both patterns are bank-conflict-free for
@@ -448,6 +463,12 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
 #ifndef MKID_F3_T1LDS
 #define MKID_F3_T1LDS 1
 #endif
+#ifndef MKID_F3_TWREG
+#define MKID_F3_TWREG 1
+#endif
+#ifndef MKID_F3_PAIRRING
+#define MKID_F3_PAIRRING 1
+#endif
 template <int N>
 struct G3 {
     static constexpr int NW = N / 512;
@@ -535,7 +556,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 const int64_t hop = h0 + g + qh;
                 if (hop > h0 + 2 * T - 2 + F) continue;
                 const uint4 v = load4<N>(a, h0 + g, tid);
+#if MKID_F3_PAIRRING
+                ring3_put(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
+#else
                 ring_put<N>(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
+#endif
             }
         }
         uint2 tq[8];
@@ -546,6 +571,17 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
         const float2* t2 = tw2 + la;
         int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);   // slot of hop k - 2T + 1
         __syncthreads();
+#if MKID_F3_TWREG
+        // the lane's 14 twiddles are the same every iteration: held in VGPRs (the transform path
+        // has registers to spare), 14 fewer LDS reads per sub-FFT on an LDS that is ~60 % busy
+        float2 w1[7], w2[7];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            w1[k - 1] = t1[64 * (k - 1)];
+            w2[k - 1] = t2[8 * (k - 1)];
+            asm volatile("" : "+v"(w1[k - 1].x), "+v"(w1[k - 1].y), "+v"(w2[k - 1].x), "+v"(w2[k - 1].y));
+        }
+#endif
         for (int t = 0; t <= nit; ++t) {
             STAMP3(0);
             if (t < nit) {
@@ -556,17 +592,39 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 int sb = rb + slot;
                 sb -= sb >= RS ? RS : 0;
                 float2 v[8];
+#if MKID_F3_PAIRRING
+                uint32_t xr[8][T];
+#pragma unroll
+                for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+                    for (int tau = 0; tau < T; ++tau) {
+                        int sl = sb + 2 * tau + hi;
+                        sl -= sl >= RS ? RS : 0;
+                        const uint32_t* pl = ring + sl * M + w * (M / NW) + 2 * L;
+                        const uint2 p01 = *reinterpret_cast<const uint2*>(pl);
+                        const uint2 p23 = *reinterpret_cast<const uint2*>(pl + 128);
+                        xr[4 * hi + 0][tau] = p01.x;
+                        xr[4 * hi + 1][tau] = p01.y;
+                        xr[4 * hi + 2][tau] = p23.x;
+                        xr[4 * hi + 3][tau] = p23.y;
+                    }
+#endif
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
+                    uint32_t x4[T];
+#if MKID_F3_PAIRRING
+#pragma unroll
+                    for (int tau = 0; tau < T; ++tau) x4[tau] = xr[r][tau];
+#else
                     const int hi = r >> 2;
                     const int pos = w * (M / NW) + 64 * (r & 3) + L;
-                    uint32_t x4[T];
 #pragma unroll
                     for (int tau = 0; tau < T; ++tau) {
                         int sl = sb + 2 * tau + hi;
                         sl -= sl >= RS ? RS : 0;
                         x4[tau] = ring[sl * M + pos];
                     }
+#endif
                     const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
                     const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
                     const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);
@@ -579,7 +637,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 }
                 dft<8>(v);
 #pragma unroll
+#if MKID_F3_TWREG
+                for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], w1[k - 1]);
+#else
                 for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t1[64 * (k - 1)]);
+#endif
 #if MKID_F3_T1LDS
                 t1_lds(v, reg, L);
 #else
@@ -587,7 +649,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
 #endif
                 dft<8>(v);
 #pragma unroll
+#if MKID_F3_TWREG
+                for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], w2[k - 1]);
+#else
                 for (int k = 1; k < 8; ++k) v[k] = MKID_CMUL(v[k], t2[8 * (k - 1)]);
+#endif
                 float2* t2w = reg + 72 * kl + la;
                 const float2* t2r = reg + 72 * kl + 9 * la;
 #pragma unroll
@@ -604,7 +670,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 int ws = rb + 2 * T - 1 + F + qh;
                 ws -= ws >= RS ? RS : 0;
                 ws -= ws >= RS ? RS : 0;
+                #if MKID_F3_PAIRRING
+                ring3_put(ring + ws * M, qoff, pre);
+#else
                 ring_put<N>(ring + ws * M, qoff, pre);
+#endif
                 rb += F;
                 rb -= rb >= RS ? RS : 0;
             }

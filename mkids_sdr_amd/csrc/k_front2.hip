@@ -469,6 +469,54 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
 #ifndef MKID_F3_PAIRRING
 #define MKID_F3_PAIRRING 1
 #endif
+// MKID_F3_DECOUPLE: no workgroup barrier in the loop. The transform waves meet each other through an
+// LDS arrival counter (the ring refill of iteration t is read by all of them in t + 1) and the two
+// groups hand Y over through a second one, on THREE Y buffers: transform t may run while the select
+// waves are still on t - 2, so a slow wave of one group no longer stalls the other every iteration
+// (stamps with the barrier: both groups waited ~700-900 cycles per iteration at ~3.0k of work).
+#ifndef MKID_F3_DECOUPLE
+#define MKID_F3_DECOUPLE 0
+#endif
+
+#ifndef MKID_F3_SLEEP
+#define MKID_F3_SLEEP 1
+#endif
+// LDS progress words. The transform waves share one arrival counter: a wave starts iteration t only
+// once it reads 8 t, so no transform wave is more than one iteration ahead of another and "counter
+// >= 8 t" means every one of them finished t - 1. The select waves never wait on each other, so a
+// sum would let a fast one cover for a slow one: each publishes its own completed-iteration count
+// and the transform waves wait for all eight. A wave's LDS reads and writes complete (lgkmcnt(0))
+// before its lane 0 publishes; waiters look every 64 clocks (s_sleep 1).
+__device__ __forceinline__ void lds_publish_wait() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt / expcnt untouched
+}
+__device__ __forceinline__ void lds_arrive(uint32_t* c, int lane) {
+    lds_publish_wait();
+    if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish(uint32_t* c, int lane, uint32_t v) {
+    lds_publish_wait();
+    if (lane == 0) __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* c, uint32_t target) {
+    for (;;) {
+        const uint32_t v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)v) >= target) break;
+        __builtin_amdgcn_s_sleep(MKID_F3_SLEEP);
+    }
+    asm volatile("" ::: "memory");
+}
+// every one of the 8 words c[0..7] >= target (lane l looks at c[l & 7])
+__device__ __forceinline__ void lds_wait_all8_ge(const uint32_t* c, int lane, uint32_t target) {
+    for (;;) {
+        const uint32_t v = __hip_atomic_load(c + (lane & 7), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_ballot_w64(v >= target) == ~0ull) break;
+        __builtin_amdgcn_s_sleep(MKID_F3_SLEEP);
+    }
+    asm volatile("" ::: "memory");
+}
+
 template <int N>
 struct G3 {
     static constexpr int NW = N / 512;
@@ -482,9 +530,11 @@ struct G3 {
     static constexpr int REG = 576;
     static constexpr int FB = NW * REG;
     static constexpr size_t off_fbuf = (size_t)RS * M * 4;
-    static constexpr size_t off_tw1 = off_fbuf + (size_t)2 * F * FB * 8;
+    static constexpr int NB = MKID_F3_DECOUPLE ? 3 : 2;   // Y buffers
+    static constexpr size_t off_tw1 = off_fbuf + (size_t)NB * F * FB * 8;
     static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;
-    static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
+    static constexpr size_t off_cnt = off_tw2 + (size_t)7 * 8 * 8;
+    static constexpr size_t lds_bytes = off_cnt + 64;   // [0] transform arrivals, [8..15] select
     static_assert(N == 2048 && F == 2 && CPT == 2 && F * M == FW * 64 * 4, "k_front3 geometry");
     static_assert(lds_bytes <= 160 * 1024, "LDS");
 };
@@ -512,11 +562,15 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
     float2* fbuf = reinterpret_cast<float2*>(smem + G::off_fbuf);
     float2* tw1 = reinterpret_cast<float2*>(smem + G::off_tw1);
     float2* tw2 = reinterpret_cast<float2*>(smem + G::off_tw2);
+    [[maybe_unused]] uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + G::off_cnt);
 
     const int tid = threadIdx.x;
     const int L = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool xform = wave < G::FW;
+    constexpr int SW = G::BT / 64 - G::FW;            // select waves
+    static_assert(SW == 8, "one progress word per select wave");
+    if (tid < 16) cnt[tid] = 0;                       // visible after the prologue barrier
 
     for (int i = tid; i < 7 * 64; i += G::BT) {
         const int k = i / 64 + 1, l = i % 64;
@@ -545,9 +599,20 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
 #ifndef MKID_F3_PRIO_S
 #define MKID_F3_PRIO_S 0
 #endif
+// MKID_F3_PRIO_Y / _SY: priority of the YOUNGER transform waves (4-7) / select waves (12-15). Waves i,
+// i + 4, i + 8, i + 12 share a SIMD and issue is arbitrated by age: stamps show waves 4-7 at ~3.5k
+// work cycles per iteration against ~2.75k for 0-3 (select: 12-15 ~3.1k, 8-11 ~2.5k), and the barrier
+// waits for the slowest
+#ifndef MKID_F3_PRIO_Y
+#define MKID_F3_PRIO_Y 0
+#endif
+#ifndef MKID_F3_PRIO_SY
+#define MKID_F3_PRIO_SY 0
+#endif
     if (xform) {
         // ---------------- transform waves: PFB + 512-point sub-FFT of (frame slot, w) ----------
         if (MKID_F3_PRIO_X) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_X);
+        if (MKID_F3_PRIO_Y && wave >= G::FW / 2) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_Y);
         const int slot = wave / NW, w = wave % NW;
         const int qh = (tid * 4) / M, qoff = (tid * 4) % M;   // this thread's ring write
         {   // prologue: hops k_start-2T+1 .. k_start+F-1
@@ -582,13 +647,19 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
             asm volatile("" : "+v"(w1[k - 1].x), "+v"(w1[k - 1].y), "+v"(w2[k - 1].x), "+v"(w2[k - 1].y));
         }
 #endif
-        for (int t = 0; t <= nit; ++t) {
+        for (int t = 0; t < nit + (MKID_F3_DECOUPLE ? 0 : 1); ++t) {
             STAMP3(0);
             if (t < nit) {
                 const int kr = -kLpfHist + F * t;
                 // the hops iteration t + 1 adds: loaded now, written after this wave's PFB
                 const uint4 pre = load4<N>(a, k_b + kr + F, tid);
-                float2* reg = fbuf + ((t & 1) * F + slot) * G::FB + w * G::REG;
+#if MKID_F3_DECOUPLE
+                STAMP3(6);
+                if (t > 0) lds_wait_ge(cnt, G::FW * t);             // every ring refill of t - 1 landed
+                if (t >= 3) lds_wait_all8_ge(cnt + 8, L, t - 2);     // Y buffer t % 3 read by select t - 2
+                STAMP3(7);
+#endif
+                float2* reg = fbuf + ((t % G::NB) * F + slot) * G::FB + w * G::REG;
                 int sb = rb + slot;
                 sb -= sb >= RS ? RS : 0;
                 float2 v[8];
@@ -679,12 +750,17 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 rb -= rb >= RS ? RS : 0;
             }
             STAMP3(1);
+#if MKID_F3_DECOUPLE
+            lds_arrive(cnt, L);
+#else
             __syncthreads();
+#endif
             STAMP3(2);
         }
     } else {
         // ---------------- select waves: channels st + SPT q, one iteration behind ---------------
         if (MKID_F3_PRIO_S) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_S);
+        if (MKID_F3_PRIO_SY && wave >= G::FW + SW / 2) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_SY);
         const int st = tid - G::FW * 64;
         float2 tl[CPT][NW - 1];
         int yoff[CPT];
@@ -718,7 +794,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
         float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
         int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
         __syncthreads();
-        for (int t = 0; t <= nit; ++t) {
+        for (int t = MKID_F3_DECOUPLE ? 1 : 0; t <= nit; ++t) {
             STAMP3(3);
             if (t > 0) {
                 const int kr = -kLpfHist + F * (t - 1);
@@ -730,10 +806,15 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                     for (int q = 0; q < CPT; ++q) lov[f][q] = row[st + G::SPT * q];
                 }
                 lrow += F;
+#if MKID_F3_DECOUPLE
+                STAMP3(8);
+                lds_wait_ge(cnt, G::FW * t);                        // transform t - 1 wrote Y
+                STAMP3(9);
+#endif
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
                     const int kf = kr + f;
-                    const float2* yf = fbuf + (((t - 1) & 1) * F + f) * G::FB;
+                    const float2* yf = fbuf + (((t - 1) % G::NB) * F + f) * G::FB;
                     float2 z[CPT];
 #pragma unroll
                     for (int q = 0; q < CPT; ++q) {
@@ -786,7 +867,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 }
             }
             STAMP3(4);
+#if MKID_F3_DECOUPLE
+            lds_publish(cnt + 8 + (wave - G::FW), L, (uint32_t)t);
+#else
             __syncthreads();
+#endif
             STAMP3(5);
         }
         if (a.ysum)

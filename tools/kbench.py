@@ -59,10 +59,24 @@ def main():
 
     chans = []
     for i, spec in enumerate(args.libs):
-        path, _, front = spec.partition(':')  # lib.so[:split]
+        path, _, front = spec.partition(':')  # lib.so[#a][:split]
+        path, _, order = path.partition('#')  # '#a' / '#b': relabelled feedline; '#VAR=VAL': env at create
+        env_set = None
+        if '=' in order:
+            env_set = order.split('=', 1)
+            os.environ[env_set[0]] = env_set[1]
+            order = ''
         ch = Channelizer(C, max_chunk=S, sample_rate=fs, lib_path=os.path.abspath(path),
                          front=front or 'auto')
-        ch.set_bins(feed['dds']['bins'])
+        # '#a': the same feedline with its channels relabelled in tools/lds_assign.py slot order
+        perm = np.arange(C)
+        if order == 'a':
+            from tools.lds_assign import slot_order
+            perm = slot_order(feed['dds']['bins'], C)
+        elif order == 'b':
+            from tools.lds_assign import slot_order_blocks
+            perm = slot_order_blocks(feed['dds']['bins'], C=C)
+        ch.set_bins(np.asarray(feed['dds']['bins'])[perm])
         ch.set_lpf(lpf)
         ch.set_fir(np.tile(mf, (C, 1)))
         if i == 0:
@@ -72,9 +86,13 @@ def main():
             ch.process_device(x, S, phase, d_ev, cap, d_cnt)
             torch.cuda.synchronize()
             mi, mq = ch.avg_iq()
-            dds = lut.define_dds_lut(feed['f_rf'], feed['f_base'], C, fs, phase=np.arctan2(mq, mi))
+            cal = np.arctan2(mq, mi)
+        dds = lut.define_dds_lut(list(np.asarray(feed['f_rf'])[perm]), feed['f_base'], C, fs, phase=cal[perm])
+        assert np.array_equal(np.asarray(dds['bins']) % N, np.asarray(feed['dds']['bins'])[perm] % N)
         ch.set_dds(dds['lut_i'], dds['lut_q'])
         ch.set_thresholds(np.full(C, -3000, np.int32))
+        if env_set:
+            del os.environ[env_set[0]]
         chans.append(ch)
     times = {p: {} for p in args.libs}
     for r in range(args.rounds + 1):

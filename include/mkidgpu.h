@@ -97,6 +97,13 @@ int mkid_set_stream(mkid_ctx* ctx, void* hip_stream);
 int mkid_set_pfb(mkid_ctx* ctx, const float* coeffs, int32_t n);
 /* Host-only (no device needed): the effective taps h_q * 2^-S of mkid_set_pfb and S. */
 int mkid_pfb_effective_taps(const float* coeffs, int32_t T, int32_t N, float* out, int32_t* shift);
+/* Host-only: the channel order the N = 2048 front end (k_front3) gives its select threads for a
+ * bin set (the C = 2048 order of the same scheme is reported too; k_front4 does not use it): out[st + (C/2) q] = channel read by thread st in instruction q.
+ * Each wave keeps its own 128 channels; within them the order puts each half-wave's 32 Y reads on
+ * distinct LDS bank pairs where the bins allow. A permutation of 0..C-1 (the identity for C other
+ * than 1024 and 2048). Results do not depend on it: each channel's arithmetic is unchanged.
+ * Exposed for tests and tools/lds_assign.py; MKID_SLOT_ORDER=0 at context creation disables it. */
+int mkid_slot_order(const int32_t* bins, int32_t C, int16_t* out);
 
 /* Coarse FFT bin per channel: replaces write_int('bins'), write_int('load_bins',(i<<1)+1)
  * (ROACH_Setup.py:534-550; ROACH_Pulses.py:958-974). bins[c] in [0,N). */

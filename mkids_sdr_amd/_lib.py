@@ -75,6 +75,7 @@ _SIGS = {
     'mkid_set_stream': [P, P],
     'mkid_set_pfb': [P, P, I32],
     'mkid_pfb_effective_taps': [P, I32, I32, P, P],
+    'mkid_slot_order': [P, I32, P],
     'mkid_set_bins': [P, P, I32],
     'mkid_set_dds': [P, P, P, I32],
     'mkid_set_lpf': [P, P, I32],

@@ -567,7 +567,25 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
     const int tid = threadIdx.x;
     const int L = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+// k_front3's raw / phase stores: plain. With the slot order a wave's store instruction covers its
+// 64 channels' positions within 2 (raw) or 4 (phase) lines in any lane order; non-temporal partial
+// lines cost k_front3 +1.3 % and the trigger that reads them back +10 % (A/B
+// profiles/r03_h_kbench_f3_slot_order2.json), plain ones are merged in L2
+#ifndef MKID_F3_NT_STORES
+#define MKID_F3_NT_STORES 0
+#endif
+#ifndef MKID_F3_INTERLEAVE
+#define MKID_F3_INTERLEAVE 0
+#endif
+#if MKID_F3_INTERLEAVE
+    // roles alternate by age on each SIMD (waves i, i+4, i+8, i+12 share one): transform waves
+    // 0-3 and 8-11, select waves 4-7 and 12-15
+    const bool xform = ((wave >> 2) & 1) == 0;
+    const int rw = (wave & 3) | ((wave >> 3) << 2);   // index within its role
+#else
     const bool xform = wave < G::FW;
+    const int rw = xform ? wave : wave - G::FW;
+#endif
     constexpr int SW = G::BT / 64 - G::FW;            // select waves
     static_assert(SW == 8, "one progress word per select wave");
     if (tid < 16) cnt[tid] = 0;                       // visible after the prologue barrier
@@ -612,15 +630,16 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
     if (xform) {
         // ---------------- transform waves: PFB + 512-point sub-FFT of (frame slot, w) ----------
         if (MKID_F3_PRIO_X) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_X);
-        if (MKID_F3_PRIO_Y && wave >= G::FW / 2) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_Y);
-        const int slot = wave / NW, w = wave % NW;
-        const int qh = (tid * 4) / M, qoff = (tid * 4) % M;   // this thread's ring write
+        if (MKID_F3_PRIO_Y && rw >= G::FW / 2) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_Y);
+        const int slot = rw / NW, w = rw % NW;
+        const int xt = rw * 64 + L;                            // thread index among the transform waves
+        const int qh = (xt * 4) / M, qoff = (xt * 4) % M;      // this thread's ring write
         {   // prologue: hops k_start-2T+1 .. k_start+F-1
             const int64_t h0 = k_start - 2 * T + 1;
             for (int g = 0; g < 2 * T - 1 + F; g += 2) {
                 const int64_t hop = h0 + g + qh;
                 if (hop > h0 + 2 * T - 2 + F) continue;
-                const uint4 v = load4<N>(a, h0 + g, tid);
+                const uint4 v = load4<N>(a, h0 + g, xt);
 #if MKID_F3_PAIRRING
                 ring3_put(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
 #else
@@ -652,7 +671,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
             if (t < nit) {
                 const int kr = -kLpfHist + F * t;
                 // the hops iteration t + 1 adds: loaded now, written after this wave's PFB
-                const uint4 pre = load4<N>(a, k_b + kr + F, tid);
+                const uint4 pre = load4<N>(a, k_b + kr + F, xt);
 #if MKID_F3_DECOUPLE
                 STAMP3(6);
                 if (t > 0) lds_wait_ge(cnt, G::FW * t);             // every ring refill of t - 1 landed
@@ -760,14 +779,20 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
     } else {
         // ---------------- select waves: channels st + SPT q, one iteration behind ---------------
         if (MKID_F3_PRIO_S) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_S);
-        if (MKID_F3_PRIO_SY && wave >= G::FW + SW / 2) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_SY);
-        const int st = tid - G::FW * 64;
+        if (MKID_F3_PRIO_SY && rw >= SW / 2) __builtin_amdgcn_s_setprio(MKID_F3_PRIO_SY);
+        const int st = rw * 64 + L;
         float2 tl[CPT][NW - 1];
         int yoff[CPT];
         float ic[CPT], qc[CPT];
+        // channel of (thread, q): a host-chosen order (mkid_api.hip slot_order) that puts the 32
+        // channels each half-wave reads per instruction on distinct LDS bank pairs of Y, each
+        // wave keeping its own 128 channels (stores and LO loads stay within 2-4 lines)
+        int cq[CPT];
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) cq[q] = a.slot_ch ? (int)a.slot_ch[st + G::SPT * q] : st + G::SPT * q;
 #pragma unroll
         for (int q = 0; q < CPT; ++q) {
-            const int c = st + G::SPT * q;
+            const int c = cq[q];
             const int32_t bin = a.bins[c];
 #pragma unroll
             for (int u = 1; u < NW; ++u) {
@@ -803,7 +828,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 for (int f = 0; f < F; ++f) {
                     const float2* row = a.lo + ((lrow + f) & (a.P - 1)) * C;
 #pragma unroll
-                    for (int q = 0; q < CPT; ++q) lov[f][q] = row[st + G::SPT * q];
+                    for (int q = 0; q < CPT; ++q) lov[f][q] = row[cq[q]];
                 }
                 lrow += F;
 #if MKID_F3_DECOUPLE
@@ -842,13 +867,13 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                             const int jr = (kf - 1) >> 1;
 #pragma unroll
                             for (int q = 0; q < CPT; ++q) {
-                                const int c = st + G::SPT * q;
+                                const int c = cq[q];
                                 ys[q].x += y[q].x;
                                 ys[q].y += y[q].y;
                                 const float ph = phase_atan2(y[q].y - qc[q], y[q].x - ic[q]);
                                 int qv = __float2int_rn(ph * 8192.0f);
                                 qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
-#if MKID_NT_STORES
+#if MKID_F3_NT_STORES
 #ifndef MKID_XP_STAMPS
                                 if (phase_run) __builtin_nontemporal_store(ph, phase_run + jr * C + c);
 #endif
@@ -868,7 +893,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
             }
             STAMP3(4);
 #if MKID_F3_DECOUPLE
-            lds_publish(cnt + 8 + (wave - G::FW), L, (uint32_t)t);
+            lds_publish(cnt + 8 + rw, L, (uint32_t)t);
 #else
             __syncthreads();
 #endif
@@ -876,7 +901,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
         }
         if (a.ysum)
 #pragma unroll
-            for (int q = 0; q < CPT; ++q) ysum_add(a.ysum, st + G::SPT * q, ys[q].x, ys[q].y);
+            for (int q = 0; q < CPT; ++q) ysum_add(a.ysum, cq[q], ys[q].x, ys[q].y);
     }
 }
 

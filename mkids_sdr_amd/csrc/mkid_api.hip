@@ -146,6 +146,10 @@ struct mkid_ctx {
     // bin-parity sign of K4 folded in: P is even, so the sign depends on k mod P only)
     std::vector<float2> h_lo;      // [P][C]
     std::vector<int32_t> h_bins;   // [C]
+    // select-slot order of the N = 2048 front end (k_front3): d_slot_ch[slot] = channel (slot_order
+    // below; MKID_SLOT_ORDER=0 keeps the identity)
+    int16_t* d_slot_ch = nullptr;
+    bool slot_order_on = true;
     // replay-trigger workspace (lazy, grown on demand)
     uint32_t* d_rflags = nullptr;
     double* d_rmeans = nullptr;
@@ -224,7 +228,7 @@ static void free_all(mkid_ctx* c) {
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
                     c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff,
-                    c->d_live,  c->d_phist, c->d_phist_tmp};
+                    c->d_live,  c->d_phist, c->d_phist_tmp, c->d_slot_ch};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -312,6 +316,7 @@ static int quantize_pfb(const float* h, int T, int N, std::vector<int16_t>& hq) 
 }
 
 static int upload_lo_folded(mkid_ctx* c);
+static int upload_slot_order(mkid_ctx* c);
 static int upload_pfb(mkid_ctx* c, const float* coeffs);
 
 extern "C" {
@@ -358,6 +363,8 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
         c->front_v2 = c->fused && front2_supported(N) && !(v1 && atoi(v1) != 0);
         const char* v3 = getenv("MKID_FRONT_V3");
         c->front_variant = (v3 && atoi(v3) == 0) ? 2 : 3;
+        const char* so = getenv("MKID_SLOT_ORDER");
+        c->slot_order_on = !(so && atoi(so) == 0);
     }
     // split front end: a large call is cut into 4 sub-chunks so the channeliser (stream A) of
     // sub-chunk i+1 overlaps the low-pass/trigger (stream B) of sub-chunk i
@@ -461,6 +468,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_reruns, C);
     AL(d_counts, 2);
     AL(d_live, C);
+    AL(d_slot_ch, C);
 #undef AL
     // defaults: identity bins, unit LO, Blackman 250 kHz low-pass, zero matched filter (no
     // triggers), zero centres, thresholds off, EMA baseline alpha=41 gate=8192.
@@ -484,7 +492,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->h_lo = lo;
     c->h_bins = bins;
     *out = c;
-    if (upload_pfb(c, h.data()) != MKID_OK || mkid_reset_stream(c) != MKID_OK) {
+    if (upload_pfb(c, h.data()) != MKID_OK || upload_slot_order(c) != MKID_OK || mkid_reset_stream(c) != MKID_OK) {
         g_err = c->err;
         free_all(c);
         delete c;
@@ -566,6 +574,8 @@ int mkid_set_bins(mkid_ctx* c, const int32_t* bins, int32_t n) {
     int r = upload(c, c->d_bins, b.data(), (size_t)n * 4);
     if (r) return r;
     c->h_bins = b;
+    r = upload_slot_order(c);
+    if (r) return r;
     return upload_lo_folded(c);
 }
 
@@ -581,6 +591,88 @@ int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
         }
     c->h_lo = std::move(lo);
     return upload_lo_folded(c);
+}
+
+// The select threads of k_front3 (C = 1024) and k_front4 (C = 2048) read Y at entry
+// yswz(bin & 511) of each sub-FFT region (regions and frames are 0 mod 32 entries apart), so a
+// channel's LDS bank pair is that entry mod 32; a ds_read_b64 costs one LDS cycle per distinct
+// address on the busiest pair of each 32-lane half (MI355X_MICROARCH.md §LDS). Slot
+// st + (C/2) q (st = 64 w + 32 h + l) is read by lane 32 h + l of wave w in instruction q; wave w
+// owns channels 128 w .. 128 w + 127 and reads them in four groups of 32. In channel order random
+// bins cost ~3.4 cycles per group. Greedy per wave: its channels by pair-class size, each into the
+// group whose cost rises least, then whose new cost is lowest, then the emptiest: ~1.9 cycles per
+// group (tools/lds_assign.py holds the same algorithm and its model).
+// k_front4 (C = 2048) has the same read pattern but loses with the order (+0.5 % with plain stores,
+// +2.6 % with its non-temporal ones: profiles/r03_h_kbench_f4_slot_order.json), so only k_front3
+// takes it; mkid_slot_order still reports the C = 2048 order for the model and tests.
+static void slot_order(const std::vector<int32_t>& bins, int C, std::vector<int16_t>& out) {
+    out.resize(C);
+    for (int i = 0; i < C; ++i) out[i] = (int16_t)i;
+    if (C != 1024 && C != 2048) return;
+    constexpr int B = 128, NG = 4, GS = 32;
+    auto yoff = [](int b) { const int k = b & 511; return k ^ ((k >> 2) & 14); };
+    for (int w = 0; w < C / B; ++w) {
+        int cnt[32] = {0};
+        int yo[B];
+        for (int i = 0; i < B; ++i) {
+            yo[i] = yoff(bins[B * w + i]);
+            ++cnt[yo[i] & 31];
+        }
+        std::vector<int> order(B);
+        for (int i = 0; i < B; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+            const int ka = yo[a] & 31, kb = yo[b] & 31;
+            if (cnt[ka] != cnt[kb]) return cnt[ka] > cnt[kb];
+            if (ka != kb) return ka < kb;
+            return yo[a] < yo[b];
+        });
+        int size[NG] = {0}, gmax[NG] = {0}, mult[NG][32] = {{0}};
+        std::vector<int> seen[NG];
+        int member[NG][GS];
+        for (int i : order) {
+            const int k = yo[i] & 31;
+            int bg = -1, bk0 = 0, bk1 = 0, bk2 = 0;
+            bool bsame = false;
+            for (int g = 0; g < NG; ++g) {
+                if (size[g] >= GS) continue;
+                const bool same = std::find(seen[g].begin(), seen[g].end(), yo[i]) != seen[g].end();
+                const int m = mult[g][k] + (same ? 0 : 1);
+                const int nm = std::max(gmax[g], m);
+                const int k0 = nm - gmax[g], k1 = nm, k2 = size[g];
+                if (bg < 0 || k0 < bk0 || (k0 == bk0 && (k1 < bk1 || (k1 == bk1 && k2 < bk2)))) {
+                    bg = g; bk0 = k0; bk1 = k1; bk2 = k2; bsame = same;
+                }
+            }
+            member[bg][size[bg]++] = B * w + i;
+            if (!bsame) {
+                seen[bg].push_back(yo[i]);
+                ++mult[bg][k];
+            }
+            gmax[bg] = std::max(gmax[bg], mult[bg][k]);
+        }
+        for (int g = 0; g < NG; ++g)
+            for (int l = 0; l < GS; ++l) out[64 * w + 32 * (g & 1) + l + (C / 2) * (g >> 1)] = (int16_t)member[g][l];
+    }
+}
+
+static int upload_slot_order(mkid_ctx* c) {
+    std::vector<int16_t> so;
+    if (c->slot_order_on) {
+        slot_order(c->h_bins, c->C, so);
+    } else {
+        so.resize(c->C);
+        for (int i = 0; i < c->C; ++i) so[i] = (int16_t)i;
+    }
+    return upload(c, c->d_slot_ch, so.data(), so.size() * 2);
+}
+
+int mkid_slot_order(const int32_t* bins, int32_t C, int16_t* out) {
+    if (!bins || !out || C <= 0) return MKID_E_ARG;
+    std::vector<int32_t> b(bins, bins + C);
+    std::vector<int16_t> so;
+    slot_order(b, C, so);
+    std::copy(so.begin(), so.end(), out);
+    return MKID_OK;
 }
 
 // d_lo[p][c] = h_lo[p][c] * (-1)^(b_c (k+1)) for any frame k = p (mod P): odd bins flip the sign
@@ -838,6 +930,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
         fa.variant = c->front_variant;
+        fa.slot_ch = c->N == 2048 ? c->d_slot_ch : nullptr;   // k_front3 only (k_front4: A/B lost)
         tstart(c, MKID_K_FRONT, &kt, A);
         HIPCHK(c, front4_supported(N) ? launch_front4(fa, A)
                                       : (c->front_v2 ? launch_front2(N, fa, A) : launch_front(N, fa, A)));

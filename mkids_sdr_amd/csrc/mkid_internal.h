@@ -98,6 +98,7 @@ struct FrontArgs {
     int16_t* iqtap;         // [K/2][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
     int32_t iq_ch;
     int32_t variant;        // N = 2048: 3 = wave-specialised k_front3, else k_front2
+    const int16_t* slot_ch; // [C] k_front3: channel of select slot st + 512 q (nullptr: identity)
 };
 
 struct TrigSpecArgs {

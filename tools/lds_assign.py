@@ -54,16 +54,18 @@ def assign(yoff, ng=32, gs=32):
 
 
 def slot_order(bins, C=1024):
-    """slot -> channel for k_front3's select waves: slot st + 512 q (st = 64 w + 32 h + l) is
-    lane l of half h of select wave w, read instruction q; group index g = (q, w, h)."""
+    """slot -> channel for the select threads: slot st + (C/2) q (st = 64 w + 32 h + l) is lane l
+    of half h of wave w, read instruction q (k_front3: C = 1024, 8 select waves; k_front4: C = 2048,
+    16 waves); group index g = (q, w, h)."""
     bins = np.asarray(bins)
     yoff = np.array([yswz(int(b) & 511) for b in bins])
-    groups = assign(yoff)
+    ng = C // 32
+    groups = assign(yoff, ng=ng)
     perm = np.empty(C, np.int64)
     for g, members in enumerate(groups):
-        q, w, h = g // 16, (g // 2) % 8, g % 2
+        q, w, h = g // (ng // 2), (g // 2) % (ng // 4), g % 2
         for l, c in enumerate(members):
-            perm[64 * w + 32 * h + l + 512 * q] = c
+            perm[64 * w + 32 * h + l + (C // 2) * q] = c
     return perm
 
 
@@ -80,13 +82,14 @@ def slot_order_blocks(bins, B=128, C=1024):
         for j, members in enumerate(groups):
             for l, c in enumerate(members):
                 # group j of wave blk: read instruction q = j >> 1, half h = j & 1
-                slot = 64 * blk + 32 * (j & 1) + l + 512 * (j >> 1)
+                slot = 64 * blk + 32 * (j & 1) + l + (C // 2) * (j >> 1)
                 perm[slot] = ch[c]
     return perm
 
 
 def natural_groups(C=1024):
-    return [[64 * w + 32 * h + l + 512 * q for l in range(32)] for q in range(2) for w in range(8) for h in range(2)]
+    return [[64 * w + 32 * h + l + (C // 2) * q for l in range(32)] for q in range(2) for w in range(C // 128)
+            for h in range(2)]
 
 
 if __name__ == '__main__':
@@ -99,3 +102,7 @@ if __name__ == '__main__':
         print('natural %d  assigned %d  per-wave blocks %d  (ideal 32 cycles per 32 group-reads)' % (
             group_cost(natural_groups(), yoff), group_cost(natural_groups(), yoff[perm]),
             group_cost(natural_groups(), yoff[pb])))
+    bins = rng.permutation(np.arange(1, 4096))[:2048]
+    yoff = np.array([yswz(int(b) & 511) for b in bins])
+    print('C = 2048: natural %d  assigned %d' % (group_cost(natural_groups(2048), yoff),
+                                                group_cost(natural_groups(2048), yoff[slot_order(bins, 2048)])))

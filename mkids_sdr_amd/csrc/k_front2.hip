@@ -57,6 +57,9 @@
 #ifndef MKID_CMUL
 #define MKID_CMUL cmul_pk
 #endif
+#ifndef MKID_F2_PAIRRING
+#define MKID_F2_PAIRRING 1
+#endif
 #ifndef MKID_F2_T1LDS
 #define MKID_F2_T1LDS 1
 #endif
@@ -193,6 +196,31 @@ __device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
     hop[3 * Q + a] = v.w;
 }
 
+// the same paired plane layout for any NW (every plane is Q = M / NW = 256 samples): samples
+// qoff..qoff+3 of a hop go to plane (o mod NW), plane index o / NW (qoff is a multiple of 4, so the
+// 4 indices of a plane stay in one 64-block and ring3_idx steps by 2)
+template <int N>
+__device__ __forceinline__ void ring_put_paired(uint32_t* hop, int qoff, uint4 v) {
+    using G = G2<N>;
+    constexpr int Q = G::M / G::NW;
+    static_assert(Q == 256, "paired plane layout");
+    if constexpr (G::NW == 1) {
+        const int a = ring3_idx(qoff);
+        hop[a] = v.x;
+        hop[a + 2] = v.y;
+        hop[a + 4] = v.z;
+        hop[a + 6] = v.w;
+    } else if constexpr (G::NW == 2) {
+        const int a = ring3_idx(qoff / 2);
+        hop[a] = v.x;
+        hop[a + 2] = v.z;
+        hop[Q + a] = v.y;
+        hop[Q + a + 2] = v.w;
+    } else {
+        ring3_put(hop, qoff, v);
+    }
+}
+
 // T1 through the wave's own LDS region instead of DPP/permlane moves: element (lane 8 kl + la,
 // register r) goes to (lane 8 r + la, register kl). Lane L writes register r at 72 r + L; lane L'
 // reads register r' at 72 (L' >> 3) + 8 r' + (L' & 7). Both patterns are bank-conflict-free for
@@ -284,7 +312,11 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
             const int64_t hop = h0 + g + qh;
             if (hop > h0 + RS - 1) continue;
             const uint4 v = load4<N>(a, h0 + g, tid);
+#if MKID_F2_PAIRRING
+            ring_put_paired<N>(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
+#else
             ring_put<N>(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
+#endif
         }
     }
     __syncthreads();
@@ -332,6 +364,7 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
         int sb = rb + slot;
         sb -= sb >= RS ? RS : 0;
         float2 v[8];
+        [[maybe_unused]] uint32_t xo[T];   // MKID_F2_PAIRRING: the odd point's samples
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int hi = r >> 2;
@@ -342,12 +375,32 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
             const uint64_t h64 = *reinterpret_cast<const uint64_t*>(tp + 64 * r);
 #endif
             uint32_t x4[T];
+#if MKID_F2_PAIRRING
+            // points r, r + 1 (r even) are one ds_read_b64 of the paired plane layout: read at the
+            // even point, kept for the odd one
+            static_assert(T == 4, "taps");
+            if ((r & 1) == 0) {
+#pragma unroll
+                for (int tau = 0; tau < T; ++tau) {
+                    int sl = sb + 2 * tau + hi;
+                    sl -= sl >= RS ? RS : 0;
+                    const uint2 p = *reinterpret_cast<const uint2*>(ring + sl * M + w * (M / NW) + 128 * ((r & 3) >> 1) + 2 * L);
+                    x4[tau] = p.x;
+                    xo[tau] = p.y;
+                }
+            } else {
+#pragma unroll
+                for (int tau = 0; tau < T; ++tau) x4[tau] = xo[tau];
+            }
+            (void)pos;
+#else
 #pragma unroll
             for (int tau = 0; tau < T; ++tau) {
                 int sl = sb + 2 * tau + hi;
                 sl -= sl >= RS ? RS : 0;
                 x4[tau] = ring[sl * M + pos];
             }
+#endif
             const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
             const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
             const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);
@@ -389,7 +442,11 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
         {   // ring refill for the next iteration (its oldest FPB hops), prefetch one further
             int ws = rb + qh;
             ws -= ws >= RS ? RS : 0;
+#if MKID_F2_PAIRRING
+            ring_put_paired<N>(ring + ws * M, qoff, pre);
+#else
             ring_put<N>(ring + ws * M, qoff, pre);
+#endif
             rb += FPB;
             rb -= rb >= RS ? RS : 0;
             lrow += FPB;

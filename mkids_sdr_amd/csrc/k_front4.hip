@@ -106,9 +106,21 @@ __device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int
 // samples qoff..qoff+7 of a hop (qoff a multiple of 8) into the permuted hop layout: sample o at
 // (o % 8) Q + o / 8, i.e. one dword in each of the 8 planes (consecutive lanes, consecutive dwords)
 // (SPT = 4: samples qoff..qoff+3 go to planes qoff % 8 .. + 3; lanes 2k, 2k+1 share a bank, 2-way)
+#ifndef MKID_F4_PAIRRING
+#define MKID_F4_PAIRRING 1
+#endif
+// MKID_F4_PAIRRING: plane index i at 128 (i >> 7) + 2 (i & 63) + ((i >> 6) & 1) (k_front2.hip
+// ring3_idx), so the PFB reads points r, r + 1 of a lane with one ds_read_b64
+__device__ __forceinline__ int ring_idx4(int i) {
+#if MKID_F4_PAIRRING
+    return 128 * (i >> 7) + 2 * (i & 63) + ((i >> 6) & 1);
+#else
+    return i;
+#endif
+}
 __device__ __forceinline__ void ring_put8(uint32_t* hop, int qoff, uint4 v0, uint4 v1) {
     constexpr int Q = G4::Q;
-    uint32_t* p = hop + (qoff % 8) * Q + qoff / 8;
+    uint32_t* p = hop + (qoff % 8) * Q + ring_idx4(qoff / 8);
     p[0] = v0.x; p[Q] = v0.y; p[2 * Q] = v0.z; p[3 * Q] = v0.w;
     if constexpr (G4::SPT == 8) {
         p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
@@ -302,17 +314,34 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
             int sb = rb + sl0;
             sb -= sb >= RS ? RS : 0;
             float2 v[8];
+            [[maybe_unused]] uint32_t xo[T];   // MKID_F4_PAIRRING: the odd point's samples
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 const int hi = r >> 2;
-                const int pos = w * G::Q + 64 * (r & 3) + L;
                 uint32_t x4[T];
+#if MKID_F4_PAIRRING
+                if ((r & 1) == 0) {
+#pragma unroll
+                    for (int tau = 0; tau < T; ++tau) {
+                        int s = sb + 2 * tau + hi;
+                        s -= s >= RS ? RS : 0;
+                        const uint2 p = *reinterpret_cast<const uint2*>(ring + s * M + w * G::Q + 128 * ((r & 3) >> 1) + 2 * L);
+                        x4[tau] = p.x;
+                        xo[tau] = p.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int tau = 0; tau < T; ++tau) x4[tau] = xo[tau];
+                }
+#else
+                const int pos = w * G::Q + 64 * (r & 3) + L;
 #pragma unroll
                 for (int tau = 0; tau < T; ++tau) {
                     int s = sb + 2 * tau + hi;
                     s -= s >= RS ? RS : 0;
                     x4[tau] = ring[s * M + pos];
                 }
+#endif
                 const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
                 const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
                 const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);

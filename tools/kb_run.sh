@@ -1,5 +1,4 @@
 set -e
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u tools/kbench.py --channels 256 --log2-samples 28 --rounds 12 build/variants/f2n.so build/variants/f2p.so > gpurun_out/kb_f2p_256.json 2> gpurun_out/kb_f2p_256.err
-timeout -k 10 300 python -u tools/kbench.py --channels 512 --log2-samples 29 --rounds 10 build/variants/f2n.so build/variants/f2p.so > gpurun_out/kb_f2p_512.json 2> gpurun_out/kb_f2p_512.err
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py > gpurun_out/f2p_parity.log 2>&1
+timeout -k 10 1000 python -u -m pytest -m gpu -x -v --timeout 200 --timeout-method thread tests/ > gpurun_out/r03_i_gpu.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_i_smoke.log 2>&1

@@ -250,12 +250,6 @@ __global__ __launch_bounds__(G2<N>::BT, 4) void k_front2(FrontArgs a) {
     float2* tw1 = reinterpret_cast<float2*>(smem + G::off_tw1);
     float2* tw2 = reinterpret_cast<float2*>(smem + G::off_tw2);
 
-    // optional issue priority above a co-resident lean trigger wave (process_fused's opt-in
-    // pipeline); measured neutral-to-worse, off
-#ifndef MKID_F2_PRIO
-#define MKID_F2_PRIO 0
-#endif
-    if (MKID_F2_PRIO) __builtin_amdgcn_s_setprio(MKID_F2_PRIO);
     const int tid = threadIdx.x;
     const int L = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -257,173 +257,6 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
     a.counts[sc] = n;
 }
 
-// ---- lean variant for the fused pipeline (process_fused): the front end holds 4 waves x 112
-// VGPRs (k_front2) or 2 x 224 (k_front4) of every SIMD's 512, so a trigger wave of <= 64 VGPRs
-// stays resident beside it and issues in the front end's stall cycles. Same recurrence and
-// outputs as k_trig_spec (EMA / no baseline, states past the start-of-stream hold-off), with
-// wave-uniform matched-filter taps (kernel arguments, SGPR operands) and a 13-register window:
-//   Q_k = (raw_{2k+1} | raw_{2k} << 16), slot k mod 13 (segments start at multiples of 26)
-//   odd  j = 2k+1: f = sum_{m<13} dot2((a_2m, a_2m+1), Q_{k-m})
-//   even j = 2k:   f = a_0 raw_2k + sum_{m<12} dot2((a_2m+1, a_2m+2), Q_{k-1-m}) + a_25 lo(Q_{k-13})
-// (integer sums: exact in any order). Packets are assembled inline (a call would pin the live
-// values in callee-saved registers around it). ----
-
-struct LeanWin {
-    uint32_t Q[kFirTaps / 2];
-    uint32_t last, sel;
-};
-
-// window for a segment starting at row j0 (a multiple of 26): Q_{j0/2 - d}, d = 1..13, in slot 13 - d
-// (d = 13 in slot 0); rows below 0 come from the carried history (older: 0, only its unused half)
-__device__ __forceinline__ void lean_load(LeanWin& w, const TrigSpecArgs& a, int c, int64_t j0) {
-    auto rawv = [&](int64_t jj) -> int32_t {
-        return jj >= 0 ? a.raw[jj * a.C + c] : (jj >= -kRawHist ? a.rhist[(jj + kRawHist) * a.C + c] : 0);
-    };
-#pragma unroll
-    for (int d = 1; d <= kFirTaps / 2; ++d) {
-        const int64_t k2 = j0 - 2 * d;   // Q_{j0/2-d} = (raw_{k2+1}, raw_{k2})
-        w.Q[(kFirTaps / 2 - d) % (kFirTaps / 2)] = pack2(rawv(k2 + 1), rawv(k2));
-    }
-    const int32_t r1 = rawv(j0 - 1);
-    w.last = pack2(r1, r1);
-    w.sel = (c & 1) ? 0x07060302u : 0x05040100u;
-}
-
-// f at group position u (j = 26 g + u), r the aligned dword holding raw_j
-template <int U>
-__device__ __forceinline__ int32_t lean_mf(LeanWin& w, const TrigSpecArgs& a, uint32_t r, bool live) {
-    constexpr int H = kFirTaps / 2;
-    const uint32_t qj = __builtin_amdgcn_perm(w.last, r, w.sel);   // (raw_j, raw_{j-1})
-    w.last = r;
-    int32_t acc;
-    if constexpr (U & 1) {
-        constexpr int k = (U - 1) / 2;
-        w.Q[k] = qj;
-        acc = 0;
-#pragma unroll
-        for (int m = 0; m < H; ++m)
-            acc = __builtin_amdgcn_sdot2(as_s2(a.utap[m]), as_s2(w.Q[(k - m + 2 * H) % H]), acc, false);
-    } else {
-        constexpr int k = U / 2;
-        acc = __builtin_amdgcn_sdot2(as_s2(a.utap0), as_s2(qj), 0, false);
-#pragma unroll
-        for (int m = 0; m < H - 1; ++m)
-            acc = __builtin_amdgcn_sdot2(as_s2(a.utapb[m]), as_s2(w.Q[(k - 1 - m + 2 * H) % H]), acc, false);
-        acc = __builtin_amdgcn_sdot2(as_s2(a.utap25), as_s2(w.Q[k % H]), acc, false);
-    }
-    return live ? mf_out(acc) : 0;
-}
-
-// The packet of make_packet in 32-bit arithmetic (bit-identical for filtered samples, which are
-// int16): |d| = |y3 - y1| <= 65535 so d^2 fits uint32, |8 den| <= 2^20; C's truncating int64
-// division of a non-negative numerator is the magnitude quotient with the divisor's sign.
-__device__ __forceinline__ uint64_t lean_packet(int32_t c, int32_t y1, int32_t y2, int32_t y3, int32_t base,
-                                                uint32_t jm1) {
-    const int32_t den = y3 + y1 - 2 * y2;
-    int32_t peak = y2;
-    if (den != 0) {
-        const int32_t d = y3 - y1;
-        const uint32_t q = ((uint32_t)d * (uint32_t)d) / (uint32_t)(8 * (den < 0 ? -den : den));
-        peak = den < 0 ? y2 + (int32_t)q : y2 - (int32_t)q;
-    }
-    const uint32_t pk = (uint32_t)tclampi((peak >> 4) + 2048, 0, 4095);
-    const uint32_t bs = (uint32_t)tclampi((base >> 4) + 2048, 0, 4095);
-    const uint32_t hi = ((uint32_t)(c & 0xFFF) << (MKID_PKT_CH_SHIFT - 32)) | (pk << (MKID_PKT_PEAK_SHIFT - 32)) |
-                        (bs >> (32 - MKID_PKT_BASE_SHIFT));
-    const uint32_t lo = (bs << MKID_PKT_BASE_SHIFT) | (jm1 & (uint32_t)MKID_PKT_TS_MASK);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-template <int U, class F>
-__device__ __forceinline__ void lean_unroll(F&& f) {
-    if constexpr (U < kFirTaps) {
-        f(std::integral_constant<int, U>{});
-        lean_unroll<U + 1>(f);
-    }
-}
-
-template <int MODE>
-__global__ __launch_bounds__(kSpecThreads, 8) void k_trig_lean(TrigSpecArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * kSpecThreads + threadIdx.x;
-    if (g >= (int64_t)a.C * a.nseg) return;
-    const int C = a.C;
-    const int c = (int)(g % C);
-    const int s = __builtin_amdgcn_readfirstlane((int)(g / C));  // 64 | C: one segment per wave
-    const bool live = a.live[c] != 0;
-    const TrigCfg k{a.thr[c], MODE, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
-    const int64_t seg0 = (int64_t)s * a.L;   // L and W are multiples of 26 (plan_sub)
-    const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
-    const int64_t jw = (s == 0 || seg0 <= a.W) ? 0 : seg0 - a.W;
-    LeanWin win;
-    lean_load(win, a, c, jw);
-    const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
-    uint64_t* slot = a.slots + sc * a.capseg;
-    int32_t n = 0;
-    const char* base = reinterpret_cast<const char*>(a.raw + (int64_t)__builtin_amdgcn_readfirstlane((int32_t)jw) * C);
-    const uint32_t loff = (uint32_t)(c >> 1) * 4u;
-    const uint32_t row = (uint32_t)(2 * C);
-    auto ld = [&](uint32_t off) { return *reinterpret_cast<const uint32_t*>(base + off + loff); };
-    int32_t f0;
-    {   // the first sample's f seeds a guessed baseline (trig_update's binit branch)
-        LeanWin w0 = win;
-        f0 = lean_mf<0>(w0, a, ld(0), live);
-    }
-    const TrigState st0 = jw == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
-    Stepper<MODE> sp(st0, k, f0);
-    // the configuration is wave-uniform (kernel arguments): keep it in SGPRs
-    sp.q.alpha = __builtin_amdgcn_readfirstlane(sp.q.alpha);
-    sp.q.dx = __builtin_amdgcn_readfirstlane(sp.q.dx);
-    sp.q.goff = __builtin_amdgcn_readfirstlane(sp.q.goff);
-    sp.q.glim = __builtin_amdgcn_readfirstlane(sp.q.glim);
-    uint32_t goff = 0;
-    const uint32_t jlo = (uint32_t)(a.j0 + jw);   // stamps are taken mod 2^28
-    // rows [jw + 26 g0, jw + 26 g1): 13-dword rolling prefetch (slot u refilled with sample u of
-    // the next half group as it is consumed)
-    auto groups = [&](auto outc, int32_t ngroups, int64_t jrow0) {
-        constexpr bool out = decltype(outc)::value;
-        constexpr int H = kFirTaps / 2;
-        uint32_t r[H];
-        if (ngroups <= 0) return;
-#pragma unroll
-        for (int u = 0; u < H; ++u) r[u] = ld(goff + (uint32_t)u * row);
-        for (int32_t gr = 0; gr < ngroups; ++gr) {
-            const uint32_t nxt = goff + (gr + 1 < ngroups ? (uint32_t)kFirTaps * row : 0u);
-            lean_unroll<0>([&](auto uc) {
-                constexpr int u = decltype(uc)::value;
-                const uint32_t v = r[u % H];
-                r[u % H] = ld((u < H ? goff + (uint32_t)(H + u) * row : nxt + (uint32_t)(u - H) * row));
-                const int32_t f = lean_mf<u>(win, a, v, live);
-                EvInfo ev;
-                if (sp.step(f, ev) && out) {   // warm-up: state only (out = false)
-                    if (n < a.capseg)
-                        slot[n] = lean_packet(c, ev.y1, ev.y2, f, ev.base, jlo + (uint32_t)(jrow0 - jw) + (uint32_t)(gr * kFirTaps + u - 1));
-                    ++n;
-                }
-            });
-            goff += (uint32_t)kFirTaps * row;
-        }
-    };
-    groups(std::false_type{}, __builtin_amdgcn_readfirstlane((int32_t)(seg0 - jw) / kFirTaps), jw);
-    if (s > 0) a.s_spec[(int64_t)s * C + c] = sp.state();
-    const int32_t len = (int32_t)(seg1 - seg0);
-    const int32_t full = len - len % kFirTaps;
-    groups(std::true_type{}, __builtin_amdgcn_readfirstlane(full / kFirTaps), seg0);
-    const int32_t left = len - full;   // tail < 26 samples, predicated
-    lean_unroll<0>([&](auto uc) {
-        constexpr int u = decltype(uc)::value;
-        if (u < left) {
-            const int32_t f = lean_mf<u>(win, a, ld(goff + (uint32_t)u * row), live);
-            EvInfo ev;
-            if (sp.step(f, ev)) {
-                if (n < a.capseg) slot[n] = lean_packet(c, ev.y1, ev.y2, f, ev.base, jlo + (uint32_t)(seg0 - jw + full + u - 1));
-                ++n;
-            }
-        }
-    });
-    a.s_end[(int64_t)s * C + c] = sp.state();
-    a.counts[sc] = n;
-}
-
 // Re-run segment s of channel c from the true state T and the speculative state S0 side by side.
 // Returns true if they merged; T becomes the true state at the segment end when they did not.
 __device__ bool rerun_segment(const TrigSpecArgs& a, int c, int s, const int32_t (&tap)[kFirTaps],
@@ -542,11 +375,7 @@ int64_t trigger_wave_slots(int device) {
 hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s) {
     const int64_t threads = (int64_t)a.C * a.nseg;
     const dim3 grid((unsigned)((threads + kSpecThreads - 1) / kSpecThreads));
-    if (a.live && a.mode == MKID_BASE_EMA)
-        hipLaunchKernelGGL(k_trig_lean<MKID_BASE_EMA>, grid, dim3(kSpecThreads), 0, s, a);
-    else if (a.live && a.mode == MKID_BASE_NONE)
-        hipLaunchKernelGGL(k_trig_lean<MKID_BASE_NONE>, grid, dim3(kSpecThreads), 0, s, a);
-    else if (a.mode == MKID_BASE_EMA)
+    if (a.mode == MKID_BASE_EMA)
         hipLaunchKernelGGL(k_trig_spec<MKID_BASE_EMA>, grid, dim3(kSpecThreads), 0, s, a);
     else if (a.mode == MKID_BASE_SVF)
         hipLaunchKernelGGL(k_trig_spec<MKID_BASE_SVF>, grid, dim3(kSpecThreads), 0, s, a);

@@ -108,11 +108,6 @@ struct mkid_ctx {
     hipEvent_t ev_start = nullptr, ev_done = nullptr;
     int zi = 0;
     int64_t G = 0;  // pipeline sub-chunk (samples)
-    int64_t pipe_G = 0;  // fused front end: sub-chunk of the two-stream pipeline (0 = off)
-    // matched filter as the lean trigger needs it: one tap row shared by every live channel
-    bool taps_uniform = true;
-    int16_t utaps[kFirTaps] = {0};
-    uint8_t* d_live = nullptr;      // [C] 1: the shared taps, 0: all-zero taps
     int64_t last_raw_row = 0;       // first row of the last sub-chunk's raw phase in d_raw
     bool fused = false;  // K1-K6 in one kernel (k_front / k_front2 / k_front4: no z buffers, no stream B work)
     bool front_v2 = false;  // fused front end is k_front2 (N = 512..2048; MKID_FRONT_V1=1 forces v1)
@@ -228,7 +223,7 @@ static void free_all(mkid_ctx* c) {
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
                     c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff,
-                    c->d_live,  c->d_phist, c->d_phist_tmp, c->d_slot_ch};
+                    c->d_phist, c->d_phist_tmp, c->d_slot_ch};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -377,22 +372,6 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->Kmax = G / c->M;
     c->Jmax = G / N;
     c->nsub_max = (cfg->max_chunk + G - 1) / G;
-    // fused front end, two-stream pipeline (opt-in, MKID_PIPE_MIN_CHUNK): a call of >= pipe_min
-    // samples runs as 4 sub-chunks, the front end of sub-chunk i+1 (stream A) beside the trigger of
-    // sub-chunk i (stream B, the lean variant: resident next to the front end's waves). d_raw
-    // holds the whole call, one region per sub-chunk. Off by default: measured same-box at config
-    // 3 it does not pay (5.49 ms/step without, 5.99-6.13 with, profiles/r02_v7_kbench_pipeline.json):
-    // the front end leaves too few issue cycles for the resident trigger to hide in.
-#ifndef MKID_PIPE_MIN
-#define MKID_PIPE_MIN ((int64_t)1 << 62)
-#endif
-    int64_t pipe_min = MKID_PIPE_MIN;
-    if (const char* ev = getenv("MKID_PIPE_MIN_CHUNK")) pipe_min = std::max<int64_t>(4 * N, atoll(ev));  // tests
-    if (c->fused && cfg->max_chunk >= pipe_min) {
-        c->pipe_G = cfg->max_chunk / 4;
-        c->pipe_G -= c->pipe_G % N;
-        c->nsub_max = std::max<int64_t>(c->nsub_max, (cfg->max_chunk + c->pipe_G - 1) / c->pipe_G);
-    }
     // Packet capacities are hard bounds: an event needs >= dead_time + 3 phase samples (trigger,
     // peak, dead time, re-arm), so no per-channel/segment overflow can occur.
     const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // whole call, one segment
@@ -467,7 +446,6 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_scratch, (size_t)C * c->scratch_cap);
     AL(d_reruns, C);
     AL(d_counts, 2);
-    AL(d_live, C);
     AL(d_slot_ch, C);
 #undef AL
     // defaults: identity bins, unit LO, Blackman 250 kHz low-pass, zero matched filter (no
@@ -479,15 +457,13 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     std::vector<float2> lo((size_t)C * P, make_float2(32767.f / 32768.f, 0.f));
     std::vector<int16_t> fir((size_t)C * kFirTaps, 0);
     std::vector<float> zero(C, 0.f);
-    std::vector<uint8_t> dead(C, 0);   // default matched filter: all-zero taps (uniform, none live)
     for (int i = 0; i < kFirTaps; ++i) c->lpf.g[i] = kBlackman250k[i] / 2048.0f;
     if ((e = hipMemcpy(c->d_bins, bins.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_thr, thr.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_lo, lo.data(), lo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_fir, fir.data(), fir.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_ic, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_qc, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_live, dead.data(), C, hipMemcpyHostToDevice)) != hipSuccess)
+        (e = hipMemcpy(c->d_qc, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "hipMemcpy defaults");
     c->h_lo = lo;
     c->h_bins = bins;
@@ -702,27 +678,7 @@ int mkid_set_fir(mkid_ctx* c, const int16_t* taps, int32_t nch, int32_t nt) {
     if (nch != c->C || nt != kFirTaps) FAIL(c, MKID_E_ARG, "matched filter must be [C][26]");
     for (int64_t i = 0; i < (int64_t)nch * nt; ++i)
         if (taps[i] < -2048 || taps[i] > 2047) FAIL(c, MKID_E_ARG, "matched-filter tap outside 12-bit range");
-    // uniform: every channel's row is either the first non-zero row or all zero (the reference
-    // loads one LUT file for every channel and zeroes deleted ones, ROACH_Pulses.py:59-111)
-    const int16_t* shared = nullptr;
-    std::vector<uint8_t> live((size_t)nch, 0);
-    bool uniform = true;
-    for (int ch = 0; ch < nch && uniform; ++ch) {
-        const int16_t* row = taps + (size_t)ch * nt;
-        bool zero = true;
-        for (int i = 0; i < nt; ++i) zero = zero && row[i] == 0;
-        if (zero) continue;
-        if (!shared) shared = row;
-        uniform = std::equal(row, row + nt, shared);
-        live[ch] = 1;
-    }
-    int r = upload(c, c->d_fir, taps, (size_t)nch * nt * 2);
-    if (r) return r;
-    r = upload(c, c->d_live, live.data(), (size_t)nch);
-    if (r) return r;
-    c->taps_uniform = uniform;
-    for (int i = 0; i < kFirTaps; ++i) c->utaps[i] = shared ? shared[i] : 0;
-    return MKID_OK;
+    return upload(c, c->d_fir, taps, (size_t)nch * nt * 2);
 }
 
 int mkid_set_centers(mkid_ctx* c, const float* ic, const float* qc, int32_t n) {
@@ -804,7 +760,7 @@ static SubPlan plan_sub(const mkid_ctx* c, int64_t J) {
         return p;
     }
     const bool serial = J <= kSegL;
-    // segment starts at multiples of 26 (the lean trigger's window is group-aligned)
+    // segment starts at multiples of 26 (the trigger's window ring is group-aligned)
     const int64_t Ls = serial ? J : (seg_length(J, c->C, c->trig_slots) + kFirTaps - 1) / kFirTaps * kFirTaps;
     SubPlan p;
     p.J = J;
@@ -837,7 +793,7 @@ static int plan_call(mkid_ctx* c, int64_t n, int64_t G, std::vector<SubPlan>& su
 // machine (speculative segments + fix-up) into segments seg_off.. of the call's slot table, then
 // the raw-phase history roll. Compaction (K8) runs once per call (compact_call).
 static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32_t stride, int32_t seg_off,
-                       int32_t capseg, hipStream_t s, bool lean = false) {
+                       int32_t capseg, hipStream_t s) {
     const int C = c->C;
     KTime kt;
     TrigSpecArgs ta{raw,        c->d_rhist, c->d_fir,   c->d_thr,      c->d_tstate,  c->d_tstate,
@@ -845,14 +801,6 @@ static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32
                     sp.J,       c->j0,      C,          sp.nseg,       sp.L,         sp.W,
                     capseg,     c->mode,    c->alpha,   c->kf,         c->kq,        c->base_thr,
                     c->cfg.dead_time, stride, seg_off};
-    if (lean) {
-        auto p2 = [](int16_t lo, int16_t hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); };
-        ta.live = c->d_live;
-        for (int m = 0; m < kFirTaps / 2; ++m) ta.utap[m] = p2(c->utaps[2 * m], c->utaps[2 * m + 1]);
-        for (int m = 0; m < kFirTaps / 2 - 1; ++m) ta.utapb[m] = p2(c->utaps[2 * m + 1], c->utaps[2 * m + 2]);
-        ta.utap0 = p2(c->utaps[0], 0);
-        ta.utap25 = p2(c->utaps[kFirTaps - 1], 0);
-    }
     tstart(c, MKID_K_TRIGGER, &kt, s);
     HIPCHK(c, launch_trigger(ta, s));
     tstop(c, &kt, s);
@@ -873,33 +821,22 @@ static int compact_call(mkid_ctx* c, int32_t stride, int32_t capseg, uint64_t* d
 }
 
 // Fused front end: one front-end launch per sub-chunk (ADC -> phase, raw), then K7, one
-// compaction per call. A long call (pipe_G) with a lean-eligible trigger (uniform matched-filter
-// taps, EMA / no baseline) runs as a two-stream pipeline: the front end of sub-chunk i+1 on
-// stream A while the lean trigger of sub-chunk i runs on stream B, resident beside it; every
-// sub-chunk writes its own region of d_raw, so A never waits for B inside a call. Otherwise all
-// on the context stream.
+// compaction per call, all on the context stream. (Round 2 also had an opt-in two-stream pipeline
+// running a register-lean trigger beside the front end; it never paid — the front ends keep their
+// SIMDs ~77 % VALU-busy, and the lean kernel alone is no faster than k_trig_spec — and was removed
+// in round 3: profiles/r02_v7_kbench_pipeline.json, r03_h_kbench_trig_lean_standalone*.json.)
 static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
                          int64_t cap, int64_t* d_counts) {
     const int C = c->C, N = c->N, M = c->M;
-    // k_front4 (2 waves/SIMD, latency bound) is slowed more by a resident trigger wave than the
-    // trigger's time is worth (config 5: 8.6 -> 11.6 ms/step measured), so only k_front2 pipelines
-    const bool pipe = c->pipe_G > 0 && n > c->pipe_G && c->taps_uniform && c->front_v2 &&
-                      (c->mode == MKID_BASE_EMA || c->mode == MKID_BASE_NONE);
-    // the lean trigger has no start-of-stream hold-off path: every state is past it once more
-    // than kHoldOff rows have been processed since the reset
-    const int64_t G = pipe ? c->pipe_G : c->G;
-    hipStream_t A = c->stream, B = pipe ? c->sB : c->stream;
+    const int64_t G = c->G;
+    hipStream_t A = c->stream;
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
     {
         int r = plan_call(c, n, G, subs, stride, capseg);
         if (r) return r;
     }
-    if (pipe) {   // B joins A's order (inputs written by earlier work on A, previous calls)
-        HIPCHK(c, hipEventRecord(c->ev_start, A));
-        HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
-    }
-    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, B));
+    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, A));
     HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, A));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
@@ -935,13 +872,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         HIPCHK(c, front4_supported(N) ? launch_front4(fa, A)
                                       : (c->front_v2 ? launch_front2(N, fa, A) : launch_front(N, fa, A)));
         tstop(c, &kt, A);
-        if (pipe) {
-            HIPCHK(c, hipEventRecord(c->ev_zready[si & 1], A));
-            HIPCHK(c, hipStreamWaitEvent(B, c->ev_zready[si & 1], 0));
-        }
-        // the last sub-chunk's trigger runs alone: the regular kernel, which fills the GPU
-        const bool last = off + S >= n;
-        int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, B, pipe && !last && c->j0 > kHoldOff);
+        int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, A);
         if (r) return r;
         seg_off += subs[si].nseg;
         c->k0 += K;
@@ -951,15 +882,11 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         c->last_raw_row = off / N;
     }
     {
-        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, B);
+        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, A);
         if (r) return r;
     }
     HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, c->H, n, 4, A));
     HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)c->H * 4, hipMemcpyDeviceToDevice, A));
-    if (pipe) {   // ... and A (the caller's stream) waits for everything B did
-        HIPCHK(c, hipEventRecord(c->ev_done, B));
-        HIPCHK(c, hipStreamWaitEvent(A, c->ev_done, 0));
-    }
     c->iq_rows = c->iq_ch >= 0 ? n / N : 0;
     return MKID_OK;
 }

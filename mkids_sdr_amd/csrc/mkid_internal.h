@@ -121,13 +121,6 @@ struct TrigSpecArgs {
     // the segments of one call's sub-chunks share one [C][seg_stride] slot table, so that a single
     // compaction at the end of the call orders packets channel-major over the whole call
     int32_t seg_stride, seg_off;
-    // lean variant (k_trig_lean, when live != nullptr): per-channel live flags (0: all-zero
-    // taps) and the shared taps as int16 pairs: utap[m] = (a_2m, a_2m+1), utapb[m] = (a_2m+1,
-    // a_2m+2), utap0 = (a_0, 0), utap25 = (a_25, 0)
-    const uint8_t* live;
-    uint32_t utap[kFirTaps / 2];
-    uint32_t utapb[kFirTaps / 2 - 1];
-    uint32_t utap0, utap25;
 };
 
 struct HeightArgs {

@@ -305,13 +305,12 @@ def test_iq_snapshot_tap_matches_oracle(gpu, front):
     (256, 2 ** 18, None, 33, 0, False),
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 34, 1, True),       # fused N = 2048, deleted channels
 ])
-def test_fused_two_stream_pipeline(gpu, monkeypatch, C, S, splits, seed, mode, deleted):
-    """process_fused's pipeline (front end of sub-chunk i+1 on stream A beside the lean trigger of
-    sub-chunk i on stream B; forced here at small sizes with MKID_PIPE_MIN_CHUNK) against the
-    oracle: uniform matched-filter taps (zero rows = deleted channels), EMA and no-baseline modes,
-    streamed calls (the first sub-chunk after the reset runs the regular trigger, the rest the
-    lean one)."""
-    monkeypatch.setenv('MKID_PIPE_MIN_CHUNK', str(8 * 2 * C))
+def test_fused_deleted_channels_and_modes(gpu, C, S, splits, seed, mode, deleted):
+    """The fused front end + trigger against the oracle with uniform matched-filter taps whose
+    zero rows are deleted channels (the reference zeroes a deleted channel's LUT,
+    ROACH_Pulses.py:59-111), EMA and no-baseline modes, streamed calls. (Round 2 ran these cases
+    through an opt-in two-stream pipeline with a register-lean trigger; both were removed in round
+    3 as measured not to pay)"""
     case = signals.make_case(C, S, seed=seed, pulses_per_ch=max(2.0, S / (2 * C) / 400))
     if deleted:
         case.fir12[1::3] = 0

@@ -1,0 +1,529 @@
+// k_front5: the fused front end for N = 4096 (2048 channels, BASELINE config 5) with WAVE
+// SPECIALISATION, the k_front3 scheme (k_front2.hip) re-fitted to a 4096-point frame.
+//
+// k_front4 runs every wave through both phases of an iteration (PFB + sub-FFTs, barrier, select /
+// DDC / low-pass / phase, barrier) and keeps the FFT working set and two channels' low-pass state
+// live together in 128 VGPRs (17-21 dwords spilled); stamps show the SIMDs idling through both
+// barrier phases (VALU active 45 %). Here the two phases run in different waves, one iteration
+// apart, so each SIMD always holds waves of both kinds:
+//   * waves 0-3 transform: wave r computes sub-FFTs r and r + 4 (512 points each, in-wave, as in
+//     k_front3) of frame k and writes them to Y buffer t & 1;
+//   * waves 4-15 select frame k - 1 from buffer (t - 1) & 1: waves 4-11 three channels per thread
+//     (c = st + 512 q), waves 12-15 two (c = 1536 + st' + 256 q), so every SIMD carries one
+//     transform wave and select work for 512 channels;
+//   * one frame per iteration (the LDS does not hold two frames' Y twice at N = 4096): ring of
+//     2T + 1 = 9 hops (frame k reads hops k-7 .. k, the transform waves write the prefetched hop
+//     k + 1 over hop k - 8), Y [2][8][576] float2, one workgroup barrier per frame;
+//   * the select threads' state lives in registers only in the select waves, so the 13 complex
+//     low-pass accumulators of three channels (78 VGPRs) no longer share the file with the FFT.
+// LDS: ring 72 KiB + Y 72 KiB + the channels' avgIQ sums 16 KiB = 160 KiB (the twiddles are
+// computed into the transform lanes' VGPRs, and the select threads' avgIQ sums live in LDS, so
+// that three channels' low-pass state fits beside the select working set in 128 VGPRs).
+// Arithmetic (PFB int16 dot products, radix-8 sub-FFTs, Horner combine in W_N^{bin} joined by
+// W_N^{4 bin}, DDC, transposed decimating low-pass, atan2, Fix16_13) is k_front4's, operation for
+// operation, so the two kernels give the same outputs.
+#include "fft_common.h"
+#include "mkid_internal.h"
+
+#include <type_traits>
+
+#ifdef MKID_XP_STAMPS
+// timing-only build: lane 0 of every wave of workgroups 0-3 stamps s_memtime at points of
+// iterations (frames) 8..15 into a.phase (tools/stamps4.py ... v5); the phase output is garbage
+#define STAMP5(t_, slot_)                                                                         \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        const uint64_t tm_ = __builtin_amdgcn_s_memtime();                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        if (blockIdx.x < 4 && (t_) >= 40 && (t_) < 48 && (threadIdx.x & 63) == 0)                 \
+            reinterpret_cast<uint64_t*>(a.phase)[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 +   \
+                                                  ((t_) - 40)) * 16 + (slot_)] = tm_;              \
+    } while (0)
+#else
+#define STAMP5(t_, slot_) ((void)0)
+#endif
+
+namespace mkid {
+
+namespace {
+
+struct G5 {
+    static constexpr int N = 4096, NW = 8, M = N / 2, C = N / 2, T = kPfbTaps;
+    static constexpr int BT = 1024;
+    static constexpr int FW = 4;                  // transform waves
+    static constexpr int SPW = NW / FW;           // sub-FFTs per transform wave per frame
+    static constexpr int SPT = M / (FW * 64);     // ring-refill samples per transform thread
+    static constexpr int SW = BT / 64 - FW;       // select waves
+    static constexpr int SW3 = 8;                 // select waves with 3 channels per thread
+    static constexpr int RS = 2 * T + 1;          // ring slots (hops)
+    static constexpr int Q = M / NW;              // samples per hop plane
+    static constexpr int REG = 576;               // float2 per (frame, sub-FFT) region
+    static constexpr int FB = NW * REG;           // float2 per frame
+    static constexpr int HIST = (2 * T - 1 + kLpfHist) * M;
+    static constexpr size_t off_fbuf = (size_t)RS * M * 4;
+    static constexpr size_t off_ysum = off_fbuf + (size_t)2 * FB * 8;  // [C] float2 avgIQ partial sums
+    static constexpr size_t lds_bytes = off_ysum + (size_t)C * 8;
+    static_assert(SPT == 8 && SPW * FW == NW, "geometry");
+    static_assert(SW3 * 64 * 3 + (SW - SW3) * 64 * 2 == C, "every channel has one select slot");
+    static_assert(lds_bytes <= 160 * 1024, "LDS");
+};
+
+typedef short fshort2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fshort2_t as_s2(uint32_t v) { return __builtin_bit_cast(fshort2_t, v); }
+__device__ __forceinline__ int32_t dot2_first(uint32_t h, uint32_t x) {
+    int32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(h), "v"(x));
+    return d;
+}
+
+// the 8 samples transform thread xt contributes to hop `hop` (samples 8 xt .. 8 xt + 7)
+__device__ __forceinline__ void load_hop(const FrontArgs& a, int64_t hop, int xt, uint4& v0, uint4& v1) {
+    const int64_t s0 = hop * G5::M + (int64_t)xt * G5::SPT;
+    if (s0 >= a.K * G5::M) {
+        v0 = v1 = make_uint4(0, 0, 0, 0);
+        return;
+    }
+    if (s0 >= -a.avail) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 p = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0));
+        const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0 + 4));
+        v0 = make_uint4(p.x, p.y, p.z, p.w);
+        v1 = make_uint4(q.x, q.y, q.z, q.w);
+        return;
+    }
+    const uint32_t* h = a.xhist + (s0 + a.avail + G5::HIST);
+    v0 = *reinterpret_cast<const uint4*>(h);
+    v1 = *reinterpret_cast<const uint4*>(h + 4);
+}
+
+// hop layout: sample o at plane o % 8, plane index o / 8 stored at ring_idx(o / 8), the paired
+// plane layout of k_front3 / k_front4 (plane entries 64 apart adjacent, so a lane's PFB points
+// r, r + 1 are one ds_read_b64)
+__device__ __forceinline__ int ring_idx(int i) { return 128 * (i >> 7) + 2 * (i & 63) + ((i >> 6) & 1); }
+__device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 v1) {
+    constexpr int Q = G5::Q;
+    uint32_t* p = hop + ring_idx(xt);
+    p[0] = v0.x; p[Q] = v0.y; p[2 * Q] = v0.z; p[3 * Q] = v0.w;
+    p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
+}
+
+__device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
+// element i of a uniform float array as a 32-bit lane offset from the (SGPR) base
+__device__ __forceinline__ float ldf(const float* base, int i) {
+    return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (uint32_t)i * 4u);
+}
+
+template <int BANKS>
+__device__ __forceinline__ float upd_ror8(float old, float src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                 __builtin_bit_cast(int, src), 0x128, 0xf,
+                                                                 BANKS, false));
+}
+// T1 in registers (register bits <-> lane bits 3-5 by DPP row_ror:8 and permlane16/32 swaps): no
+// LDS round trip on the transform waves' critical path (MKID_F5_T1LDS=0)
+[[maybe_unused]] __device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
+#pragma unroll
+    for (int r0 = 0; r0 < 8; r0 += 2) {
+        const float2 a0 = v[r0], a1 = v[r0 + 1];
+        v[r0].x = upd_ror8<0xC>(a0.x, a1.x);
+        v[r0].y = upd_ror8<0xC>(a0.y, a1.y);
+        v[r0 + 1].x = upd_ror8<0x3>(a1.x, a0.x);
+        v[r0 + 1].y = upd_ror8<0x3>(a1.y, a0.y);
+    }
+    constexpr int kP16[4] = {0, 1, 4, 5};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r0 = kP16[i];
+        const auto sx = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].x),
+                                                         __builtin_bit_cast(int, v[r0 + 2].x), false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].y),
+                                                         __builtin_bit_cast(int, v[r0 + 2].y), false, false);
+        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
+        v[r0 + 2] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
+    }
+#pragma unroll
+    for (int r0 = 0; r0 < 4; ++r0) {
+        const auto sx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].x),
+                                                         __builtin_bit_cast(int, v[r0 + 4].x), false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].y),
+                                                         __builtin_bit_cast(int, v[r0 + 4].y), false, false);
+        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
+        v[r0 + 4] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
+    }
+}
+#ifndef MKID_F5_T1LDS
+#define MKID_F5_T1LDS 1
+#endif
+
+// T1 through the wave's own LDS region (k_front2.hip t1_lds)
+__device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) reg[72 * r + L] = v[r];
+    __builtin_amdgcn_wave_barrier();
+    const float2* rd = reg + 72 * (L >> 3) + (L & 7);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = rd[8 * r];
+    __builtin_amdgcn_wave_barrier();
+}
+
+// MKID_F5_CHBAR: scheduling barrier between a select thread's channels (bounds the live reads)
+#ifndef MKID_F5_CHBAR
+#define MKID_F5_CHBAR 1
+#endif
+// MKID_F5_LOAHEAD: the select threads load a frame's LO values one frame ahead (6 more VGPRs)
+#ifndef MKID_F5_LOAHEAD
+#define MKID_F5_LOAHEAD 0
+#endif
+#ifndef MKID_F5_NT_STORES
+#define MKID_F5_NT_STORES 1
+#endif
+
+// select / DDC / low-pass / phase of CPT channels c0 + cs q per thread, frame k - 1 of iteration t
+// (the centres are re-read from global memory at each output frame and the avgIQ sums kept in LDS
+// ysl: registers go to the low-pass state)
+template <int CPT>
+__device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0, int cs,
+                                           int64_t k_b, int64_t k_start, int nrun, int nit) {
+    constexpr int C = G5::C;
+    float2 tb[CPT];   // W_N^{bin}
+    int yoff[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+        const int c = c0 + cs * q;
+        const int32_t bin = a.bins[c];
+        double sn, cn;
+        sincospi(-2.0 * (double)bin / G5::N, &sn, &cn);
+        tb[q] = make_float2((float)cn, (float)sn);
+        yoff[q] = yswz(bin & 511);
+        ysl[c] = make_float2(0.f, 0.f);
+    }
+    uint64_t gp[13];
+#pragma unroll
+    for (int m = 0; m < 13; ++m) gp[m] = tap_pair(a.taps.g[2 * m], a.taps.g[2 * m + 1]);
+    float2 acc[CPT][13];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q)
+#pragma unroll
+        for (int m = 0; m < 13; ++m) acc[q][m] = make_float2(0.f, 0.f);
+    int16_t* const raw_run = a.raw + (k_b >> 1) * C;
+    float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
+    int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
+    [[maybe_unused]] float2 lonext[CPT];
+    if (MKID_F5_LOAHEAD) {
+        const char* lorow = reinterpret_cast<const char*>(a.lo + (lrow & (a.P - 1)) * C);
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) lonext[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(c0 + cs * q) * 8u);
+    }
+    __syncthreads();   // prologue: ring written
+    __syncthreads();   // transform iteration 0 (frame k_start) wrote Y buffer 0
+    // frames in pairs (even: accumulate, odd: output), one barrier after each: frame k_start + 2p
+    // is in Y buffer 0, k_start + 2p + 1 in buffer 1 (nit is even). Unrolled by hand so the
+    // accumulators keep their registers (as a parity branch, the two paths' results met in phis that
+    // the allocator resolved with copies and ~20 spilled accumulators).
+    // the warm-up pairs (no output) and the output pairs are separate loops, so that every store of
+    // the output loop is unconditional and the waits on loads issued before it are counted exactly
+    auto pair = [&](int p, auto outc) {
+        constexpr bool OUTF = decltype(outc)::value;
+        const int kf = -kLpfHist + 2 * p;   // even
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            STAMP5(2 * p + 1 + f, 8);
+            // channel base re-defined every frame so per-channel addresses are rebuilt in the loop
+            // (a few VALU) instead of being hoisted as 64-bit pointers that crowd the low-pass state
+            int cb = c0;
+            asm volatile("" : "+v"(cb));
+            const float2* yf = fbuf + f * G5::FB;
+            // LO values one frame ahead (the global-load latency hides behind a frame of work); the
+            // centres of an output frame are loaded at its start
+            float2 lov[CPT];
+#if MKID_F5_LOAHEAD
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) lov[q] = lonext[q];
+            {
+                const char* lorow = reinterpret_cast<const char*>(a.lo + ((lrow + f + 1) & (a.P - 1)) * C);
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) lonext[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
+            }
+#else
+            {
+                const char* lorow = reinterpret_cast<const char*>(a.lo + ((lrow + f) & (a.P - 1)) * C);
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) lov[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
+            }
+#endif
+            [[maybe_unused]] float icv[CPT], qcv[CPT];
+            if (f == 1) {
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) {
+                    icv[q] = ldf(a.ic, cb + cs * q);
+                    qcv[q] = ldf(a.qc, cb + cs * q);
+                }
+            }
+            auto zq = [&](int q) {
+                const float2 lo = lov[q];
+                const float2* yq = yf + yoff[q];
+                // two 4-term Horner chains in W_N^{bin}, reads in two halves (8 VGPRs of reads in flight)
+                float2 Xl = yq[3 * G5::REG], Xh = yq[7 * G5::REG];
+                float2 y2 = yq[2 * G5::REG], y6 = yq[6 * G5::REG];
+                Xl = cmac(y2, Xl, tb[q]);
+                Xh = cmac(y6, Xh, tb[q]);
+                __builtin_amdgcn_sched_barrier(0);
+                const float2 y1 = yq[G5::REG], y5 = yq[5 * G5::REG], y0 = yq[0], y4 = yq[4 * G5::REG];
+                Xl = cmac(y1, Xl, tb[q]);
+                Xh = cmac(y5, Xh, tb[q]);
+                Xl = cmac(y0, Xl, tb[q]);
+                Xh = cmac(y4, Xh, tb[q]);
+                // joined by W_N^{4 bin} = (W_N^{bin})^4 (two squarings: a few ulp, far below the phase bar)
+                const float2 t2 = cmul_pk(tb[q], tb[q]);
+                return cmul_pk(cmac(Xl, Xh, cmul_pk(t2, t2)), lo);
+            };
+            if (f == 0) {
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) {
+                    const float2 z = zq(q);
+#pragma unroll
+                    for (int m = 0; m < 13; ++m) acc[q][m] = fma_tap<1>(gp[m], z, acc[q][m]);   // g_{2m+1}
+                    if (MKID_F5_CHBAR) __builtin_amdgcn_sched_barrier(0);
+                }
+            } else {
+                const int ko = kf + 1;   // odd: output row (ko - 1) / 2 of the run
+                constexpr bool out = OUTF;   // ko > 0 && ko < nrun
+                const int jr = (ko - 1) >> 1;
+                // every channel's phase first, then the frame's stores: a load waited on after a
+                // store would wait for the store too (vmcnt retires in order)
+                float ph[CPT];
+                uint32_t iqv = 0;
+                bool iqhit = false;
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) {
+                    const float2 z = zq(q);
+                    const float2 y = fma_tap<0>(gp[0], z, acc[q][0]);                                // g_0
+#pragma unroll
+                    for (int m = 0; m < 12; ++m) acc[q][m] = fma_tap<0>(gp[m + 1], z, acc[q][m + 1]);  // g_{2m+2}
+                    acc[q][12] = make_float2(0.f, 0.f);
+                    ph[q] = phase_atan2(y.y - qcv[q], y.x - icv[q]);
+                    if (out) {
+                        const int c = cb + cs * q;
+                        // one owner per entry: a plain read-add-write (LDS float atomics ran at a small
+                        // fraction of the LDS rate and stalled every wave's LDS traffic on output frames)
+                        float2 ysv = ysl[c];
+                        ysv.x += y.x;
+                        ysv.y += y.y;
+                        ysl[c] = ysv;
+                        if (a.iqtap) {               // uniform; the IQ-tap channel's sample by select
+                            const bool hit = c == a.iq_ch;
+                            const uint32_t v = (uint32_t)(uint16_t)iq16(y.x) | ((uint32_t)(uint16_t)iq16(y.y) << 16);
+                            iqv = hit ? v : iqv;
+                            iqhit = iqhit || hit;
+                        }
+                    }
+                    if (MKID_F5_CHBAR) __builtin_amdgcn_sched_barrier(0);
+                }
+                if (out) {
+                    // uniform row bases + 32-bit lane offsets (SGPR-base stores, no 64-bit VGPR pointers)
+                    char* const prow = reinterpret_cast<char*>(phase_run + jr * C);
+                    char* const rrow = reinterpret_cast<char*>(raw_run + jr * C);
+#pragma unroll
+                    for (int q = 0; q < CPT; ++q) {
+                        const uint32_t c = (uint32_t)(cb + cs * q);
+                        int qv = __float2int_rn(ph[q] * 8192.0f);
+                        qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
+#if MKID_F5_NT_STORES
+#ifndef MKID_XP_STAMPS
+                        if (phase_run) __builtin_nontemporal_store(ph[q], reinterpret_cast<float*>(prow + c * 4u));
+#endif
+                        __builtin_nontemporal_store((int16_t)qv, reinterpret_cast<int16_t*>(rrow + c * 2u));
+#else
+#ifndef MKID_XP_STAMPS
+                        if (phase_run) *reinterpret_cast<float*>(prow + c * 4u) = ph[q];
+#endif
+                        *reinterpret_cast<int16_t*>(rrow + c * 2u) = (int16_t)qv;
+#endif
+                    }
+                    if (iqhit) *reinterpret_cast<uint32_t*>(a.iqtap + 2 * ((k_b >> 1) + jr)) = iqv;
+                }
+            }
+            STAMP5(2 * p + 1 + f, 9);
+            __syncthreads();   // Y buffer f read; the transform waves wrote the next frame into 1 - f
+            STAMP5(2 * p + 1 + f, 10);
+        }
+        lrow += 2;
+    };
+    for (int p = 0; p < kLpfHist / 2; ++p) pair(p, std::false_type{});
+    for (int p = kLpfHist / 2; p < nit / 2; ++p) pair(p, std::true_type{});
+    if (a.ysum)
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const float2 ys = ysl[c0 + cs * q];
+            ysum_add(a.ysum, c0 + cs * q, ys.x, ys.y);
+        }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
+    using G = G5;
+    constexpr int NW = G::NW, M = G::M, T = G::T, RS = G::RS;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
+    float2* fbuf = reinterpret_cast<float2*>(smem + G::off_fbuf);
+    float2* ysl = reinterpret_cast<float2*>(smem + G::off_ysum);
+
+    const int tid = threadIdx.x;
+    const int L = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const int64_t k_b = (int64_t)blockIdx.x * a.frames_per_block;
+    int64_t k_e = k_b + a.frames_per_block;
+    if (k_e > a.K) k_e = a.K;
+    if (k_b >= k_e) return;
+    const int64_t k_start = k_b - kLpfHist;
+    const int nrun = (int)(k_e - k_b);
+    const int nit = nrun + kLpfHist;                 // iterations: frames k_start .. k_e - 1 (even)
+
+#ifdef MKID_XP_STAMPS
+    uint64_t* const bst = reinterpret_cast<uint64_t*>(a.phase) + 8192 + 4 * blockIdx.x;   // per-block stamps
+    if (tid == 0) {
+        bst[0] = __builtin_amdgcn_s_memtime();
+        bst[2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+    }
+#endif
+    if (wave < G::FW) {
+        // ---------------- transform waves: sub-FFTs rw + FW s of frame k_start + t ----------------
+        const int rw = wave, xt = tid;               // xt: thread among the transform waves
+        {   // prologue: hops k_start-2T+1 .. k_start -> ring (slot = hop mod RS)
+            const int64_t h0 = k_start - 2 * T + 1;
+            for (int g = 0; g < 2 * T; ++g) {
+                uint4 v0, v1;
+                load_hop(a, h0 + g, xt, v0, v1);
+                ring_put(ring + (int)((((h0 + g) % RS) + RS) % RS) * M, xt, v0, v1);
+            }
+        }
+        uint2 tq[G::SPW][8];
+#pragma unroll
+        for (int s = 0; s < G::SPW; ++s)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) tq[s][r] = a.pfbq[NW * (64 * r + L) + rw + G::FW * s];
+        const int la = L & 7, kl = L >> 3;
+        int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);   // slot of hop k - 2T + 1
+        __syncthreads();
+        // the lane's stage-1 / stage-2 twiddles W_512^{L k}, W_64^{la k} (the same every frame)
+        float2 w1[7], w2[7];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            double sn, cn;
+            sincospi(-2.0 * (double)(L * k) / 512.0, &sn, &cn);
+            w1[k - 1] = make_float2((float)cn, (float)sn);
+            sincospi(-2.0 * (double)(la * k) / 64.0, &sn, &cn);
+            w2[k - 1] = make_float2((float)cn, (float)sn);
+            asm volatile("" : "+v"(w1[k - 1].x), "+v"(w1[k - 1].y), "+v"(w2[k - 1].x), "+v"(w2[k - 1].y));
+        }
+        for (int t = 0; t <= nit; ++t) {
+            STAMP5(t, 0);
+            if (t < nit) {
+                const int kr = -kLpfHist + t;
+                // the hop iteration t + 1 adds: loaded now, written after this wave's PFB reads
+                uint4 pre0, pre1;
+                load_hop(a, k_b + kr + 1, xt, pre0, pre1);
+                float2* fb = fbuf + (t & 1) * G::FB;
+#pragma unroll
+                for (int s = 0; s < G::SPW; ++s) {
+                    const int w = rw + G::FW * s;
+                    float2* reg = fb + w * G::REG;
+                    uint32_t xr[8][T];
+#pragma unroll
+                    for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+                        for (int tau = 0; tau < T; ++tau) {
+                            int sl = rb + 2 * tau + hi;
+                            sl -= sl >= RS ? RS : 0;
+                            const uint32_t* pl = ring + sl * M + w * G::Q + 2 * L;
+                            const uint2 p01 = *reinterpret_cast<const uint2*>(pl);
+                            const uint2 p23 = *reinterpret_cast<const uint2*>(pl + 128);
+                            xr[4 * hi + 0][tau] = p01.x;
+                            xr[4 * hi + 1][tau] = p01.y;
+                            xr[4 * hi + 2][tau] = p23.x;
+                            xr[4 * hi + 3][tau] = p23.y;
+                        }
+                    float2 v[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const uint32_t* x4 = xr[r];
+                        const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
+                        const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
+                        const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);
+                        const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x07060302u);
+                        int32_t ai = dot2_first(tq[s][r].x, i01);
+                        ai = __builtin_amdgcn_sdot2(as_s2(tq[s][r].y), as_s2(i23), ai, false);
+                        int32_t aq = dot2_first(tq[s][r].x, q01);
+                        aq = __builtin_amdgcn_sdot2(as_s2(tq[s][r].y), as_s2(q23), aq, false);
+                        v[r] = make_float2((float)ai, (float)aq);
+                    }
+                    dft<8>(v);
+#pragma unroll
+                    for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w1[k - 1]);
+#if MKID_F5_T1LDS
+                    t1_lds(v, reg, L);
+#else
+                    t1_transpose(v);
+#endif
+                    dft<8>(v);
+#pragma unroll
+                    for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w2[k - 1]);
+                    float2* t2w = reg + 72 * kl + la;
+                    const float2* t2r = reg + 72 * kl + 9 * la;
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) t2w[9 * r] = v[r];
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = t2r[r];
+                    dft<8>(v);
+                    __builtin_amdgcn_wave_barrier();
+                    float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
+                    STAMP5(t, 1 + s);
+                }
+                // ring refill: hop k + 1 over hop k - 2T (read by no one in this iteration)
+                int ws = rb + 2 * T;
+                ws -= ws >= RS ? RS : 0;
+                ring_put(ring + ws * M, xt, pre0, pre1);
+                rb += 1;
+                rb -= rb >= RS ? RS : 0;
+            }
+            STAMP5(t, 3);
+            __syncthreads();
+            STAMP5(t, 4);
+        }
+#ifdef MKID_XP_STAMPS
+        if (tid == 0) bst[1] = __builtin_amdgcn_s_memtime();
+#endif
+    } else {
+        // ---------------- select waves, one frame behind the transform waves --------------------
+        const int sw = wave - G::FW;
+        if (sw < G::SW3)
+            select_run<3>(a, fbuf, ysl, sw * 64 + L, 512, k_b, k_start, nrun, nit);
+        else
+            select_run<2>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64 + L, 256, k_b, k_start, nrun, nit);
+    }
+}
+
+hipError_t launch_front5(const FrontArgs& a0, hipStream_t s) {
+    static std::atomic<uint64_t> attr_mask{0};
+    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front5, (int)G5::lds_bytes);
+    if (e != hipSuccess) return e;
+    FrontArgs a = a0;
+    if (a.K <= 0) return hipSuccess;
+    // one run per CU (a 2^30-sample chunk: 2048 frames per CU of MI355X's 256, the 24-frame
+    // low-pass warm-up 1.2 % of it); runs are even so that every run starts on an output row
+    const int64_t ncu = a.ncu > 0 ? a.ncu : 256;
+    int64_t fpb = a.K / ncu;
+    fpb = fpb < 64 ? 64 : (fpb > 4096 ? 4096 : fpb);
+    fpb = (fpb + 1) / 2 * 2;
+    a.frames_per_block = fpb;
+    const int64_t blocks = (a.K + fpb - 1) / fpb;
+    hipLaunchKernelGGL(k_front5, dim3((unsigned)blocks), dim3(G5::BT), G5::lds_bytes, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mkid

@@ -358,6 +358,10 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
         c->front_v2 = c->fused && front2_supported(N) && !(v1 && atoi(v1) != 0);
         const char* v3 = getenv("MKID_FRONT_V3");
         c->front_variant = (v3 && atoi(v3) == 0) ? 2 : 3;
+        if (N == 4096) {
+            const char* v5 = getenv("MKID_FRONT_V5");
+            c->front_variant = (v5 && atoi(v5) == 0) ? 4 : 5;   // k_front5 unless MKID_FRONT_V5=0
+        }
         const char* so = getenv("MKID_SLOT_ORDER");
         c->slot_order_on = !(so && atoi(so) == 0);
     }
@@ -869,7 +873,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.variant = c->front_variant;
         fa.slot_ch = c->N == 2048 ? c->d_slot_ch : nullptr;   // k_front3 only (k_front4: A/B lost)
         tstart(c, MKID_K_FRONT, &kt, A);
-        HIPCHK(c, front4_supported(N) ? launch_front4(fa, A)
+        HIPCHK(c, front4_supported(N) ? (c->front_variant == 5 ? launch_front5(fa, A) : launch_front4(fa, A))
                                       : (c->front_v2 ? launch_front2(N, fa, A) : launch_front(N, fa, A)));
         tstop(c, &kt, A);
         int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, A);

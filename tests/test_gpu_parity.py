@@ -140,12 +140,12 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     (512, 2 ** 18, None, 4, 'auto'),
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'auto'),    # config 3 geometry
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'split'),
-    (2048, 2 ** 20, [0, 3 * 2 ** 17 + 4096, 2 ** 20], 6, 'auto'),   # config 5 geometry (k_front4)
+    (2048, 2 ** 20, [0, 3 * 2 ** 17 + 4096, 2 ** 20], 6, 'auto'),   # config 5 geometry (k_front5)
     (2048, 2 ** 20, None, 6, 'split'),
 ])
 def test_chain_parity(gpu, C, S, splits, seed, front):
     """Full chain vs the oracle. 'auto' runs the fused front end (k_front3 for N = 2048, k_front2
-    for N = 512/1024, k_front4 for N = 4096, k_front for N = 128); 'split' runs k_channelize +
+    for N = 512/1024, k_front5 for N = 4096, k_front for N = 128); 'split' runs k_channelize +
     k_lpf_phase with z staged in HBM."""
     case, thr = cached_case(C, S, seed, max(1.0, S / (2 * C) / 400))
     compare(case, thr, splits or [0, S], front=front)
@@ -158,6 +158,29 @@ def test_chain_parity_front2_at_2048(gpu, monkeypatch):
     C, S = 1024, 2 ** 20
     case, thr = cached_case(C, S, 5, max(1.0, S / (2 * C) / 400))
     compare(case, thr, [0, 2 ** 19, S])
+
+
+def test_chain_parity_front4_at_4096(gpu, monkeypatch):
+    """The non-specialised k_front4 at N = 4096 (MKID_FRONT_V5=0; the default there is the
+    wave-specialised k_front5) on config 5's parity case, streamed; and the two kernels' avgIQ
+    sums (the loop-calibration accumulator) agree to fp32 rounding."""
+    from mkids_sdr_amd.channelizer import Channelizer
+    monkeypatch.setenv('MKID_FRONT_V5', '0')
+    C, S = 2048, 2 ** 20
+    case, thr = cached_case(C, S, 6, max(1.0, S / (2 * C) / 400))
+    compare(case, thr, [0, 3 * 2 ** 17 + 4096, S])
+    sums = {}
+    for v in ('0', '1'):
+        monkeypatch.setenv('MKID_FRONT_V5', v)
+        ch = Channelizer(C, max_chunk=S)
+        try:
+            configure(ch, case, thr)
+            ch.process(case.iq)
+            sums[v] = np.asarray(ch.avg_iq())
+        finally:
+            ch.close()
+    scale = np.abs(sums['0']).max()
+    assert np.abs(sums['1'] - sums['0']).max() <= 1e-5 * scale
 
 
 @pytest.mark.parametrize('mode', [0, 1, 2])

@@ -69,7 +69,7 @@ def _noise_iq(S, seed):
 @pytest.mark.gpu
 def test_heights_config5_fused(gpu):
     from mkids_sdr_amd.channelizer import Channelizer
-    C, S = 2048, 2 ** 20                       # config 5 geometry: N = 4096, fused k_front4
+    C, S = 2048, 2 ** 20                       # config 5 geometry: N = 4096, fused k_front5
     ch = Channelizer(C, max_chunk=S)
     try:
         ch.set_fir(np.tile(np.arange(26, dtype=np.int16) * 40 - 500, (C, 1)))

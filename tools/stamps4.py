@@ -32,6 +32,16 @@ SEG3 = [('transform waves: PFB + sub-FFT + ring write', 0, 1), ('transform waves
         ('select waves: loop back', 5, 'next3')]
 
 
+SEG5 = [('transform: sub-FFT 0 (ring reads .. Y write)', slice(0, 4), 0, 1, 0),
+        ('transform: sub-FFT 1 (+ ring refill)', slice(0, 4), 1, 2, 0),
+        ('transform: ring refill', slice(0, 4), 2, 3, 0),
+        ('transform: barrier wait', slice(0, 4), 3, 4, 0),
+        ('transform: loop back', slice(0, 4), 4, 'next0', 0),
+        ('select: LO + select + DDC + low-pass + output', slice(4, 16), 8, 9, 8),
+        ('select: barrier wait', slice(4, 16), 9, 10, 8),
+        ('select: loop back', slice(4, 16), 10, 'next8', 8)]
+
+
 def main():
     import torch
     from mkids_sdr_amd.channelizer import Channelizer
@@ -71,6 +81,27 @@ def main():
               ' '.join('%5.0f' % v for v in swork[:, 8:].mean(axis=(0, 2))))
         it = st[:, :8, 1:, 0] - st[:, :8, :-1, 0]
         print('%-52s %8.0f cycles' % ('iteration (2 frames)', float(np.mean(it))))
+        ch.close()
+        return
+    if len(sys.argv) > 3 and sys.argv[3] == 'v5':   # k_front5: waves 0-3 transform, 4-15 select
+        st = phase[:4 * 16 * 8 * 16 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 16)
+        for name, w, a_, b_, top in SEG5:
+            x = st[:, w]
+            d = x[:, :, 1:, top] - x[:, :, :-1, a_] if str(b_).startswith('next') else x[:, :, :, b_] - x[:, :, :, a_]
+            print('%-52s %8.0f cycles  (min %6d max %6d)' % (name, float(np.mean(d)), int(d.min()), int(d.max())))
+        it = st[:, :4, 1:, 0] - st[:, :4, :-1, 0]
+        print('%-52s %8.0f cycles' % ('iteration (1 frame)', float(np.mean(it))))
+        sw = st[:, 4:, :, 9] - st[:, 4:, :, 8]
+        print('select work per wave 4..15:', ' '.join('%5.0f' % v for v in sw.mean(axis=(0, 2))))
+        nb = (S // (N // 2) + 2047) // 2048
+        bs = phase[2 * 8192:2 * (8192 + 4 * 4096)].view(torch.int64).cpu().numpy().reshape(-1, 4)
+        bs = bs[:max(1, min(len(bs), int(sys.argv[4]) if len(sys.argv) > 4 else 256))]
+        t0 = bs[:, 0].min()
+        dur = bs[:, 1] - bs[:, 0]
+        print('blocks %d: start offset min/med/max %d/%d/%d, duration min/med/max %d/%d/%d, span %d'
+              % (len(bs), 0, int(np.median(bs[:, 0] - t0)), int((bs[:, 0] - t0).max()),
+                 int(dur.min()), int(np.median(dur)), int(dur.max()), int(bs[:, 1].max() - t0)))
+        np.save(os.path.join(ROOT, 'gpurun_out', 'f5_blocks.npy'), bs)
         ch.close()
         return
     if C == 2048:   # k_front4: 8 stamps per (wave, iteration)

@@ -73,6 +73,9 @@ def main():
         if order == 'a':
             from tools.lds_assign import slot_order
             perm = slot_order(feed['dds']['bins'], C)
+        elif order == 'c':
+            from tools.lds_assign import slot_order_f5
+            perm = slot_order_f5(feed['dds']['bins'])
         elif order == 'b':
             from tools.lds_assign import slot_order_blocks
             perm = slot_order_blocks(feed['dds']['bins'], C=C)

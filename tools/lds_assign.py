@@ -87,6 +87,30 @@ def slot_order_blocks(bins, B=128, C=1024):
     return perm
 
 
+def f5_groups():
+    """k_front5's read groups (C = 2048): waves 0-7 of the select waves read channels
+    64 w + 32 h + l + 512 q (q < 3), waves 8-11 read 1536 + 64 w' + 32 h + l + 256 q (q < 2); one group
+    per (wave, half, q)."""
+    g = [[64 * w + 32 * h + l + 512 * q for l in range(32)] for w in range(8) for h in range(2) for q in range(3)]
+    g += [[1536 + 64 * w + 32 * h + l + 256 * q for l in range(32)] for w in range(4) for h in range(2)
+          for q in range(2)]
+    return g
+
+
+def slot_order_f5(bins):
+    """natural channel -> feedline channel for a relabelled feedline whose k_front5 read groups
+    are the conflict-minimising ones (tools/kbench.py lib.so#c: the bound of the select-order
+    effect with the kernel unchanged)."""
+    bins = np.asarray(bins)
+    yoff = np.array([yswz(int(b) & 511) for b in bins])
+    groups = assign(yoff, ng=64)
+    perm = np.empty(2048, np.int64)
+    for members, slots in zip(groups, f5_groups()):
+        for c, s in zip(members, slots):
+            perm[s] = c
+    return perm
+
+
 def natural_groups(C=1024):
     return [[64 * w + 32 * h + l + (C // 2) * q for l in range(32)] for q in range(2) for w in range(C // 128)
             for h in range(2)]
@@ -106,3 +130,5 @@ if __name__ == '__main__':
     yoff = np.array([yswz(int(b) & 511) for b in bins])
     print('C = 2048: natural %d  assigned %d' % (group_cost(natural_groups(2048), yoff),
                                                 group_cost(natural_groups(2048), yoff[slot_order(bins, 2048)])))
+    print('k_front5: natural %d  assigned %d' % (group_cost(f5_groups(), yoff),
+                                                group_cost(f5_groups(), yoff[slot_order_f5(bins)])))

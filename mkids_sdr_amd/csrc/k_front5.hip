@@ -391,6 +391,9 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
     if (wave < G::FW) {
         // ---------------- transform waves: sub-FFTs rw + FW s of frame k_start + t ----------------
         const int rw = wave, xt = tid;               // xt: thread among the transform waves
+#ifdef MKID_F5_PRIO_X
+        __builtin_amdgcn_s_setprio(MKID_F5_PRIO_X);
+#endif
         {   // prologue: hops k_start-2T+1 .. k_start -> ring (slot = hop mod RS)
             const int64_t h0 = k_start - 2 * T + 1;
             for (int g = 0; g < 2 * T; ++g) {

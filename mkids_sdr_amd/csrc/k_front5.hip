@@ -170,6 +170,10 @@ __device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
 #ifndef MKID_F5_CHBAR
 #define MKID_F5_CHBAR 1
 #endif
+// MKID_F5_HORNER1: the select's 8-way combine as one Horner chain (else two chains joined by W^{4 bin})
+#ifndef MKID_F5_HORNER1
+#define MKID_F5_HORNER1 0
+#endif
 // MKID_F5_LOAHEAD: the select threads load a frame's LO values one frame ahead (6 more VGPRs)
 #ifndef MKID_F5_LOAHEAD
 #define MKID_F5_LOAHEAD 0
@@ -262,6 +266,23 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             auto zq = [&](int q) {
                 const float2 lo = lov[q];
                 const float2* yq = yf + yoff[q];
+#if MKID_F5_HORNER1
+                // one 8-term Horner chain in W_N^{bin} (7 complex MACs; the two-chain form needs
+                // W_N^{4 bin}, which costs 6 VGPRs or two squarings per channel-frame); reads in two
+                // halves (8 VGPRs of reads in flight)
+                float2 X = yq[7 * G5::REG];
+                const float2 y6 = yq[6 * G5::REG], y5 = yq[5 * G5::REG], y4 = yq[4 * G5::REG];
+                X = cmac(y6, X, tb[q]);
+                X = cmac(y5, X, tb[q]);
+                X = cmac(y4, X, tb[q]);
+                __builtin_amdgcn_sched_barrier(0);
+                const float2 y3 = yq[3 * G5::REG], y2 = yq[2 * G5::REG], y1 = yq[G5::REG], y0 = yq[0];
+                X = cmac(y3, X, tb[q]);
+                X = cmac(y2, X, tb[q]);
+                X = cmac(y1, X, tb[q]);
+                X = cmac(y0, X, tb[q]);
+                return cmul_pk(X, lo);
+#else
                 // two 4-term Horner chains in W_N^{bin}, reads in two halves (8 VGPRs of reads in flight)
                 float2 Xl = yq[3 * G5::REG], Xh = yq[7 * G5::REG];
                 float2 y2 = yq[2 * G5::REG], y6 = yq[6 * G5::REG];
@@ -276,6 +297,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                 // joined by W_N^{4 bin} = (W_N^{bin})^4 (two squarings: a few ulp, far below the phase bar)
                 const float2 t2 = cmul_pk(tb[q], tb[q]);
                 return cmul_pk(cmac(Xl, Xh, cmul_pk(t2, t2)), lo);
+#endif
             };
             if (f == 0) {
 #pragma unroll

@@ -174,6 +174,14 @@ __device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
 #ifndef MKID_F5_HORNER1
 #define MKID_F5_HORNER1 0
 #endif
+// MKID_F5_HORNER_EO: even / odd chains in W^{2 bin} joined by W^{bin} (else two chains joined by W^{4 bin})
+#ifndef MKID_F5_HORNER_EO
+#define MKID_F5_HORNER_EO 0
+#endif
+// MKID_F5_YSPLIT: a channel's eight Y reads in two scheduling halves (else all eight at once)
+#ifndef MKID_F5_YSPLIT
+#define MKID_F5_YSPLIT 1
+#endif
 // MKID_F5_LOAHEAD: the select threads load a frame's LO values one frame ahead (6 more VGPRs)
 #ifndef MKID_F5_LOAHEAD
 #define MKID_F5_LOAHEAD 0
@@ -282,13 +290,27 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                 X = cmac(y1, X, tb[q]);
                 X = cmac(y0, X, tb[q]);
                 return cmul_pk(X, lo);
+#elif MKID_F5_HORNER_EO
+                // even / odd 4-term chains in W_N^{2 bin}, joined by W_N^{bin}: depth 4, 16 VALU
+                const float2 w2 = cmul_pk(tb[q], tb[q]);
+                float2 Xe = yq[6 * G5::REG], Xo = yq[7 * G5::REG];
+                const float2 y4 = yq[4 * G5::REG], y5 = yq[5 * G5::REG];
+                Xe = cmac(y4, Xe, w2);
+                Xo = cmac(y5, Xo, w2);
+                if (MKID_F5_YSPLIT) __builtin_amdgcn_sched_barrier(0);
+                const float2 y2 = yq[2 * G5::REG], y3 = yq[3 * G5::REG], y0 = yq[0], y1 = yq[G5::REG];
+                Xe = cmac(y2, Xe, w2);
+                Xo = cmac(y3, Xo, w2);
+                Xe = cmac(y0, Xe, w2);
+                Xo = cmac(y1, Xo, w2);
+                return cmul_pk(cmac(Xe, Xo, tb[q]), lo);
 #else
                 // two 4-term Horner chains in W_N^{bin}, reads in two halves (8 VGPRs of reads in flight)
                 float2 Xl = yq[3 * G5::REG], Xh = yq[7 * G5::REG];
                 float2 y2 = yq[2 * G5::REG], y6 = yq[6 * G5::REG];
                 Xl = cmac(y2, Xl, tb[q]);
                 Xh = cmac(y6, Xh, tb[q]);
-                __builtin_amdgcn_sched_barrier(0);
+                if (MKID_F5_YSPLIT) __builtin_amdgcn_sched_barrier(0);
                 const float2 y1 = yq[G5::REG], y5 = yq[5 * G5::REG], y0 = yq[0], y4 = yq[4 * G5::REG];
                 Xl = cmac(y1, Xl, tb[q]);
                 Xh = cmac(y5, Xh, tb[q]);

@@ -113,48 +113,6 @@ __device__ __forceinline__ float ldf(const float* base, int i) {
     return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (uint32_t)i * 4u);
 }
 
-template <int BANKS>
-__device__ __forceinline__ float upd_ror8(float old, float src) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
-                                                                 __builtin_bit_cast(int, src), 0x128, 0xf,
-                                                                 BANKS, false));
-}
-// T1 in registers (register bits <-> lane bits 3-5 by DPP row_ror:8 and permlane16/32 swaps): no
-// LDS round trip on the transform waves' critical path (MKID_F5_T1LDS=0)
-[[maybe_unused]] __device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
-#pragma unroll
-    for (int r0 = 0; r0 < 8; r0 += 2) {
-        const float2 a0 = v[r0], a1 = v[r0 + 1];
-        v[r0].x = upd_ror8<0xC>(a0.x, a1.x);
-        v[r0].y = upd_ror8<0xC>(a0.y, a1.y);
-        v[r0 + 1].x = upd_ror8<0x3>(a1.x, a0.x);
-        v[r0 + 1].y = upd_ror8<0x3>(a1.y, a0.y);
-    }
-    constexpr int kP16[4] = {0, 1, 4, 5};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r0 = kP16[i];
-        const auto sx = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].x),
-                                                         __builtin_bit_cast(int, v[r0 + 2].x), false, false);
-        const auto sy = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].y),
-                                                         __builtin_bit_cast(int, v[r0 + 2].y), false, false);
-        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
-        v[r0 + 2] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
-    }
-#pragma unroll
-    for (int r0 = 0; r0 < 4; ++r0) {
-        const auto sx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].x),
-                                                         __builtin_bit_cast(int, v[r0 + 4].x), false, false);
-        const auto sy = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].y),
-                                                         __builtin_bit_cast(int, v[r0 + 4].y), false, false);
-        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
-        v[r0 + 4] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
-    }
-}
-#ifndef MKID_F5_T1LDS
-#define MKID_F5_T1LDS 1
-#endif
-
 // T1 through the wave's own LDS region (k_front2.hip t1_lds)
 __device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
 #pragma unroll
@@ -166,26 +124,8 @@ __device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
     __builtin_amdgcn_wave_barrier();
 }
 
-// MKID_F5_CHBAR: scheduling barrier between a select thread's channels (bounds the live reads)
-#ifndef MKID_F5_CHBAR
-#define MKID_F5_CHBAR 1
-#endif
-// MKID_F5_HORNER1: the select's 8-way combine as one Horner chain (else two chains joined by W^{4 bin})
-#ifndef MKID_F5_HORNER1
-#define MKID_F5_HORNER1 0
-#endif
-// MKID_F5_HORNER_EO: even / odd chains in W^{2 bin} joined by W^{bin} (else two chains joined by W^{4 bin})
-#ifndef MKID_F5_HORNER_EO
-#define MKID_F5_HORNER_EO 0
-#endif
-// MKID_F5_YSPLIT: a channel's eight Y reads in two scheduling halves (else all eight at once)
-#ifndef MKID_F5_YSPLIT
-#define MKID_F5_YSPLIT 1
-#endif
-// MKID_F5_LOAHEAD: the select threads load a frame's LO values one frame ahead (6 more VGPRs)
-#ifndef MKID_F5_LOAHEAD
-#define MKID_F5_LOAHEAD 0
-#endif
+// measured and dropped (DESIGN.md §5 k_front5): T1 in registers, LO one frame ahead, one Horner
+// chain, even/odd chains, unsplit Y reads, no barrier between channels, transform-wave priority
 #ifndef MKID_F5_NT_STORES
 #define MKID_F5_NT_STORES 1
 #endif
@@ -220,12 +160,6 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
     int16_t* const raw_run = a.raw + (k_b >> 1) * C;
     float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
     int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
-    [[maybe_unused]] float2 lonext[CPT];
-    if (MKID_F5_LOAHEAD) {
-        const char* lorow = reinterpret_cast<const char*>(a.lo + (lrow & (a.P - 1)) * C);
-#pragma unroll
-        for (int q = 0; q < CPT; ++q) lonext[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(c0 + cs * q) * 8u);
-    }
     __syncthreads();   // prologue: ring written
     __syncthreads();   // transform iteration 0 (frame k_start) wrote Y buffer 0
     // frames in pairs (even: accumulate, odd: output), one barrier after each: frame k_start + 2p
@@ -248,21 +182,11 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             // LO values one frame ahead (the global-load latency hides behind a frame of work); the
             // centres of an output frame are loaded at its start
             float2 lov[CPT];
-#if MKID_F5_LOAHEAD
-#pragma unroll
-            for (int q = 0; q < CPT; ++q) lov[q] = lonext[q];
-            {
-                const char* lorow = reinterpret_cast<const char*>(a.lo + ((lrow + f + 1) & (a.P - 1)) * C);
-#pragma unroll
-                for (int q = 0; q < CPT; ++q) lonext[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
-            }
-#else
             {
                 const char* lorow = reinterpret_cast<const char*>(a.lo + ((lrow + f) & (a.P - 1)) * C);
 #pragma unroll
                 for (int q = 0; q < CPT; ++q) lov[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
             }
-#endif
             [[maybe_unused]] float icv[CPT], qcv[CPT];
             if (f == 1) {
 #pragma unroll
@@ -274,43 +198,12 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             auto zq = [&](int q) {
                 const float2 lo = lov[q];
                 const float2* yq = yf + yoff[q];
-#if MKID_F5_HORNER1
-                // one 8-term Horner chain in W_N^{bin} (7 complex MACs; the two-chain form needs
-                // W_N^{4 bin}, which costs 6 VGPRs or two squarings per channel-frame); reads in two
-                // halves (8 VGPRs of reads in flight)
-                float2 X = yq[7 * G5::REG];
-                const float2 y6 = yq[6 * G5::REG], y5 = yq[5 * G5::REG], y4 = yq[4 * G5::REG];
-                X = cmac(y6, X, tb[q]);
-                X = cmac(y5, X, tb[q]);
-                X = cmac(y4, X, tb[q]);
-                __builtin_amdgcn_sched_barrier(0);
-                const float2 y3 = yq[3 * G5::REG], y2 = yq[2 * G5::REG], y1 = yq[G5::REG], y0 = yq[0];
-                X = cmac(y3, X, tb[q]);
-                X = cmac(y2, X, tb[q]);
-                X = cmac(y1, X, tb[q]);
-                X = cmac(y0, X, tb[q]);
-                return cmul_pk(X, lo);
-#elif MKID_F5_HORNER_EO
-                // even / odd 4-term chains in W_N^{2 bin}, joined by W_N^{bin}: depth 4, 16 VALU
-                const float2 w2 = cmul_pk(tb[q], tb[q]);
-                float2 Xe = yq[6 * G5::REG], Xo = yq[7 * G5::REG];
-                const float2 y4 = yq[4 * G5::REG], y5 = yq[5 * G5::REG];
-                Xe = cmac(y4, Xe, w2);
-                Xo = cmac(y5, Xo, w2);
-                if (MKID_F5_YSPLIT) __builtin_amdgcn_sched_barrier(0);
-                const float2 y2 = yq[2 * G5::REG], y3 = yq[3 * G5::REG], y0 = yq[0], y1 = yq[G5::REG];
-                Xe = cmac(y2, Xe, w2);
-                Xo = cmac(y3, Xo, w2);
-                Xe = cmac(y0, Xe, w2);
-                Xo = cmac(y1, Xo, w2);
-                return cmul_pk(cmac(Xe, Xo, tb[q]), lo);
-#else
                 // two 4-term Horner chains in W_N^{bin}, reads in two halves (8 VGPRs of reads in flight)
                 float2 Xl = yq[3 * G5::REG], Xh = yq[7 * G5::REG];
                 float2 y2 = yq[2 * G5::REG], y6 = yq[6 * G5::REG];
                 Xl = cmac(y2, Xl, tb[q]);
                 Xh = cmac(y6, Xh, tb[q]);
-                if (MKID_F5_YSPLIT) __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_sched_barrier(0);
                 const float2 y1 = yq[G5::REG], y5 = yq[5 * G5::REG], y0 = yq[0], y4 = yq[4 * G5::REG];
                 Xl = cmac(y1, Xl, tb[q]);
                 Xh = cmac(y5, Xh, tb[q]);
@@ -319,7 +212,6 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                 // joined by W_N^{4 bin} = (W_N^{bin})^4 (two squarings: a few ulp, far below the phase bar)
                 const float2 t2 = cmul_pk(tb[q], tb[q]);
                 return cmul_pk(cmac(Xl, Xh, cmul_pk(t2, t2)), lo);
-#endif
             };
             if (f == 0) {
 #pragma unroll
@@ -327,7 +219,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                     const float2 z = zq(q);
 #pragma unroll
                     for (int m = 0; m < 13; ++m) acc[q][m] = fma_tap<1>(gp[m], z, acc[q][m]);   // g_{2m+1}
-                    if (MKID_F5_CHBAR) __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             } else {
                 const int ko = kf + 1;   // odd: output row (ko - 1) / 2 of the run
@@ -361,7 +253,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                             iqhit = iqhit || hit;
                         }
                     }
-                    if (MKID_F5_CHBAR) __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
                 if (out) {
                     // uniform row bases + 32-bit lane offsets (SGPR-base stores, no 64-bit VGPR pointers)
@@ -435,9 +327,6 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
     if (wave < G::FW) {
         // ---------------- transform waves: sub-FFTs rw + FW s of frame k_start + t ----------------
         const int rw = wave, xt = tid;               // xt: thread among the transform waves
-#ifdef MKID_F5_PRIO_X
-        __builtin_amdgcn_s_setprio(MKID_F5_PRIO_X);
-#endif
         {   // prologue: hops k_start-2T+1 .. k_start -> ring (slot = hop mod RS)
             const int64_t h0 = k_start - 2 * T + 1;
             for (int g = 0; g < 2 * T; ++g) {
@@ -509,11 +398,7 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
                     dft<8>(v);
 #pragma unroll
                     for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w1[k - 1]);
-#if MKID_F5_T1LDS
                     t1_lds(v, reg, L);
-#else
-                    t1_transpose(v);
-#endif
                     dft<8>(v);
 #pragma unroll
                     for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w2[k - 1]);

@@ -88,3 +88,21 @@ def test_create_without_gpu_fails_loudly():
     from mkids_sdr_amd.channelizer import Channelizer
     with pytest.raises(_lib.MkidError):
         Channelizer(64)
+
+
+def test_front5_select_groups_cover_every_channel_once():
+    """k_front5's select-read groups (tools/lds_assign.f5_groups: waves 4-11 with three channels per
+    thread, 12-15 with two) hold each of the 2048 channels exactly once, and the relabel order
+    used for its conflict bound (slot_order_f5) is a permutation that does not raise the modelled
+    gather cost."""
+    import numpy as np
+    from tools.lds_assign import f5_groups, group_cost, slot_order_f5, yswz
+    g = f5_groups()
+    assert len(g) == 64 and all(len(x) == 32 for x in g)
+    assert sorted(c for x in g for c in x) == list(range(2048))
+    rng = np.random.default_rng(3)
+    bins = rng.permutation(np.arange(1, 4096))[:2048]
+    perm = slot_order_f5(bins)
+    assert sorted(perm.tolist()) == list(range(2048))
+    yoff = np.array([yswz(int(b) & 511) for b in bins])
+    assert group_cost(g, yoff[perm]) <= group_cost(g, yoff)

@@ -20,8 +20,8 @@
 // computed into the transform lanes' VGPRs, and the select threads' avgIQ sums live in LDS, so
 // that three channels' low-pass state fits beside the select working set in 128 VGPRs).
 // Arithmetic (PFB int16 dot products, radix-8 sub-FFTs, Horner combine in W_N^{bin} joined by
-// W_N^{4 bin}, DDC, transposed decimating low-pass, atan2, Fix16_13) is k_front4's, operation for
-// operation, so the two kernels give the same outputs.
+// W_N^{4 bin}, DDC, transposed decimating low-pass, atan2, Fix16_13) is k_front4's, except that
+// W_N^{4 bin} is rebuilt by two squarings (a few ulp); both are held to the same parity bars.
 #include "fft_common.h"
 #include "mkid_internal.h"
 

@@ -11,6 +11,12 @@ Prints ONE JSON line on rank 0.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,3,5}] [--baseline {ema,svf}]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+Without an external launcher (no WORLD_SIZE in the environment), `--gpus N > 1` starts N fresh
+rank processes itself (`launch_ranks`: child processes, never an exec; the parent touches no GPU)
+and relays rank 0's line — one feedline per GPU, as the reference runs one ROACH per feedline into
+one PacketMaster (PacketMaster.c:216-218, 577-625). Under an external launcher WORLD_SIZE must
+equal --gpus.
+
 Configs (BASELINE.json `configs`; the default is configs[2], the one the
 metric is quoted on):
   2  256 ch, N = 512, fs = 550 MS/s, 2^28 samples per step
@@ -63,11 +69,18 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-phase', action='store_true', help='do not materialise the phase stream')
     p.add_argument('--copy-mib', type=int, default=2048, help='stream-copy probe size (MiB)')
-    p.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
-                   help='N > 1 packet gather: RCCL on device buffers (one GPU per rank) or gloo '
-                        'through pinned host memory (ranks may share a GPU)')
+    p.add_argument('--backend', default='auto', choices=['auto', 'nccl', 'gloo'],
+                   help='packet gather: RCCL on device buffers (one GPU per rank) or gloo through '
+                        'pinned host memory (ranks may share a GPU); auto = nccl when every rank has '
+                        'a GPU of its own, else gloo (decided by each rank, before any GPU call)')
     p.add_argument('--check-gather', action='store_true',
                    help='N > 1: verify that rank 0 received every rank\'s last-step packet list unchanged')
+    p.add_argument('--force-gather', action='store_true',
+                   help='run the packet gather (process group, double-buffered slots, side-stream '
+                        'gather, barrier + max timing) even at N = 1: a world-size-1 group')
+    p.add_argument('--launch-probe', action='store_true',
+                   help='launcher check: each rank joins a gloo group, rank 0 prints the ranks\' '
+                        'environment as one JSON line; no GPU call (CPU test of launch_ranks)')
     p.add_argument('--no-witness', action='store_true',
                    help='skip the parity witness: the one-core CPU sample (the first 2^cpu-samples-log2 '
                         'samples of the step input) re-run on the GPU from a reset context and compared '
@@ -171,27 +184,125 @@ def gather_report(gather, ev_slots, cnt_slots, last, rank, world, ctrl, args):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without an external launcher: start N rank processes running this
+    script with the same arguments (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set,
+    rendezvous on 127.0.0.1), wait for them, relay rank 0's JSON line and return the exit status.
+    The parent imports no torch and never touches a GPU, and the ranks are fresh child processes
+    (no exec). If a rank fails, the others are stopped (by their own PIDs) and its status is
+    returned; rank 0 must print exactly one JSON line."""
+    import signal
+    import threading
+    port = os.environ.get('MASTER_PORT') or str(_free_port())
+    procs = []
+    lines = []
+
+    def relay(pipe):
+        for ln in pipe:
+            if ln.startswith('{'):
+                lines.append(ln.strip())
+            else:
+                sys.stderr.write(ln)
+        pipe.close()
+
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+    reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    reader.start()
+    status = 0
+    live = list(range(n))
+    while live:
+        time.sleep(0.2)
+        for r in list(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.remove(r)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                sys.stderr.write('bench.py: rank %d exited with %d; stopping the other ranks\n' % (r, rc))
+                for o in live:
+                    try:
+                        os.kill(procs[o].pid, signal.SIGTERM)
+                    except OSError:
+                        pass
+                deadline = time.time() + 20
+                for o in live:
+                    try:
+                        procs[o].wait(max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        procs[o].kill()
+                        procs[o].wait()
+                live = []
+    reader.join(timeout=30)
+    if status == 0:
+        if len(lines) != 1:
+            sys.stderr.write('bench.py: rank 0 printed %d JSON lines, expected 1\n' % len(lines))
+            return 1
+        print(lines[0], flush=True)
+    return status
+
+
+def launch_probe(world, rank):
+    """--launch-probe: join a gloo group (no GPU call) and report every rank's view of the launch."""
+    import torch.distributed as dist
+    if os.environ.get('MKID_PROBE_FAIL_RANK') == str(rank):
+        sys.exit(3)            # test hook: a rank that dies before the rendezvous
+    dist.init_process_group('gloo')
+    mine = {'rank': dist.get_rank(), 'world': dist.get_world_size(), 'env_rank': rank,
+            'local_rank': int(os.environ.get('LOCAL_RANK', '0')), 'pid': os.getpid(),
+            'ppid': os.getppid(), 'master_addr': os.environ.get('MASTER_ADDR')}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    if rank == 0:
+        print(json.dumps({'launch_probe': True, 'n_gpus': world, 'ranks': allr}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if 'WORLD_SIZE' in os.environ and world != args.gpus:
+        raise SystemExit('WORLD_SIZE=%d but --gpus %d: launch one rank per GPU' % (world, args.gpus))
+    if args.launch_probe:
+        return launch_probe(world, rank)
+    import torch
+    import torch.distributed as dist
+
     # the rank's GPU first, then the process group bound to it (RCCL communicators are created
     # for this device, not guessed from the rank)
     # device_count() does not initialise the GPU; ranks share a device only when there are more
     # ranks than GPUs (a one-GPU box rehearsing N > 1, gloo backend only: RCCL needs distinct GPUs)
     ndev = torch.cuda.device_count()
+    if args.backend == 'auto':
+        args.backend = 'nccl' if ndev >= world else 'gloo'
     gpu = local % max(ndev, 1)
     if world > 1 and args.backend == 'nccl' and world > ndev:
         raise SystemExit('%d ranks on %d GPUs: RCCL needs one GPU per rank (use --backend gloo)' % (world, ndev))
     torch.cuda.set_device(gpu)
     dev = torch.device('cuda', gpu)
     ctrl = None
-    if world > 1:
+    grouped = world > 1 or args.force_gather
+    if grouped:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        if world == 1:                          # --force-gather: a world-size-1 group
+            os.environ.setdefault('MASTER_PORT', str(_free_port()))
+            os.environ.setdefault('RANK', '0')
+            os.environ.setdefault('WORLD_SIZE', '1')
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=dev)
             ctrl = dist.new_group(backend='gloo')     # host control channel (packet counts)
@@ -284,11 +395,11 @@ def main():
 
     # packet buffers: one slot per step in flight; with N > 1 two, so that the gather of step k
     # (rank 0's PacketMaster role) overlaps step k+1's kernels (feedlines.PacketGather)
-    slots = 2 if world > 1 else 1
+    slots = 2 if grouped else 1
     ev_slots = [d_events] + [torch.empty(cap, dtype=torch.int64, device=dev) for _ in range(slots - 1)]
     cnt_slots = [d_counts] + [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(slots - 1)]
     gather = None
-    if world > 1:
+    if grouped:
         from mkids_sdr_amd.feedlines import PacketGather
         gather = PacketGather(ev_slots, cnt_slots, args.backend, dev, dst=0, ctrl_group=ctrl,
                               keep_last=args.check_gather)
@@ -316,7 +427,7 @@ def main():
         gather.flush()
     torch.cuda.synchronize(dev)
     ch.set_timing(True)
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -325,11 +436,11 @@ def main():
     if gather is not None:
         gather.flush()           # the last step's lists are on rank 0 inside the timed region
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if grouped:
         dist.barrier()
     dt = time.perf_counter() - t0
     gather_info = None
-    if world > 1:
+    if grouped:
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=ctrl)
         dt = float(tt.item())
@@ -429,7 +540,7 @@ def main():
                        'phase_materialised': not args.no_phase,
                        'pulse_heights_in_step': bool(cf['heights']),
                        'parallelism': 'feedline-per-GPU x%d%s' % (
-                           world, '' if world == 1 else ', packet gather to rank 0 over %s' % (
+                           world, '' if not grouped else ', packet gather to rank 0 over %s' % (
                                'RCCL' if args.backend == 'nccl' else 'gloo (pinned host buffers)'))},
             'per_gpu_msps': round(value / world, 1),
             'packets_per_step_rank0': ev_last,
@@ -469,7 +580,7 @@ def main():
                 out['parity'] = par
         print(json.dumps(out), flush=True)
     ch.close()
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

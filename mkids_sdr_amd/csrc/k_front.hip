@@ -55,12 +55,6 @@
 // workgroup every iteration) from L2. With default-policy streams the LO rows miss L2 on some
 // boxes and their loads stall the select stage: same-box A/B -15 % k_front, -11 % k_trigger
 // (profiles/r01_v29_kbench_nt.json). 0 restores default-policy accesses for A/B.
-#ifndef MKID_NT_LOADS
-#define MKID_NT_LOADS 1
-#endif
-#ifndef MKID_NT_STORES
-#define MKID_NT_STORES 1
-#endif
 
 namespace mkid {
 
@@ -117,15 +111,11 @@ __device__ __forceinline__ uint4 front_load(const FrontArgs& a, int64_t first_ho
     using G = FGeo<N>;
     const int64_t s0 = first_hop * G::M + (int64_t)tid * G::SPT;  // sample index in chunk
     if (s0 >= a.K * G::M) return make_uint4(0, 0, 0, 0);
-#if MKID_NT_LOADS
     if (s0 >= -a.avail) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0));
         return make_uint4(v.x, v.y, v.z, v.w);
     }
-#else
-    if (s0 >= -a.avail) return *reinterpret_cast<const uint4*>(a.x + s0);
-#endif
     return *reinterpret_cast<const uint4*>(a.xhist + (s0 + a.avail + G::HIST));
 }
 
@@ -341,17 +331,9 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
                     int q = __float2int_rn(ph * 8192.0f);
                     q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
 #ifndef MKID_XP_STAMPS
-#if MKID_NT_STORES
                     if (phase_run) __builtin_nontemporal_store(ph, phase_run + jr * C + c);
-#else
-                    if (phase_run) (phase_run + jr * C)[c] = ph;
 #endif
-#endif
-#if MKID_NT_STORES
                     __builtin_nontemporal_store((int16_t)q, raw_run + jr * C + c);
-#else
-                    (raw_run + jr * C)[c] = (int16_t)q;
-#endif
                     if (c == a.iq_ch && a.iqtap) {  // IQ snapshot tap (conv_phase_snapIQ_bram)
                         a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y.x);
                         a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y.y);

@@ -6,9 +6,9 @@
 //
 //  * a 1024-thread workgroup (16 waves, 4 per SIMD, <= 128 VGPRs) walks its run FPB = 2 frames per
 //    iteration; wave (s, w) computes sub-FFT w of frame s, thread t then owns the two channels
-//    t + 1024 q (q = 0, 1) in the select / DDC / low-pass / phase stage. (MKID_F4_BT=512: 8 waves,
-//    2 per SIMD, 4 channels per thread, no spills, 7 % slower: two waves per SIMD cannot hide the
-//    barrier phases; the 1024-thread build spills ~21 loop-invariant dwords and still wins);
+//    t + 1024 q (q = 0, 1) in the select / DDC / low-pass / phase stage. (512-thread workgroups, 8
+//    waves, 2 per SIMD, 4 channels per thread, no spills, were 7 % slower: two waves per SIMD cannot
+//    hide the barrier phases; the 1024-thread build spills ~21 loop-invariant dwords and still wins);
 //  * the PFB taps of a wave's points are the same every frame, so they live in VGPRs (8 int16
 //    quads per lane) and the LDS holds only the ADC ring (9 hops, 72 KiB), the Y buffers of the two
 //    frames (72 KiB) and the two twiddle tables: 151.5 KiB of the CU's 160 KiB;
@@ -16,15 +16,7 @@
 //    W_N^{bin} joined by W_N^{4 bin} (two complex constants per channel instead of seven);
 //  * the decimating low-pass folds its accumulator shift into the output frame's FMAs.
 // Index maps and LDS layouts are those of k_front2.hip at NW = 8 (tools/front2_layouts.py).
-#include "fft_common.h"
-#include "mkid_internal.h"
-
-#ifndef MKID_NT_LOADS
-#define MKID_NT_LOADS 1
-#endif
-#ifndef MKID_NT_STORES
-#define MKID_NT_STORES 1
-#endif
+#include "front_common.h"
 
 #ifdef MKID_XP_STAMPS
 // timing-only build: lane 0 of every wave of workgroups 0-3 stamps s_memtime at 6 points of
@@ -46,11 +38,8 @@ namespace mkid {
 
 namespace {
 
-#ifndef MKID_F4_BT
-#define MKID_F4_BT 1024
-#endif
 struct G4 {
-    static constexpr int N = 4096, NW = 8, FPB = 2, BT = MKID_F4_BT, CPT = 2048 / BT;
+    static constexpr int N = 4096, NW = 8, FPB = 2, BT = 1024, CPT = 2048 / BT;
     static constexpr int SPW = FPB * NW * 64 / BT;     // sub-FFTs per wave per iteration
     static constexpr int SPT = FPB * (N / 2) / BT;     // ring-refill samples per thread (8 or 4)
     static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
@@ -67,14 +56,6 @@ struct G4 {
     static_assert(lds_bytes <= 160 * 1024, "LDS");
 };
 
-typedef short fshort2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ fshort2_t as_s2(uint32_t v) { return __builtin_bit_cast(fshort2_t, v); }
-__device__ __forceinline__ int32_t dot2_first(uint32_t h, uint32_t x) {
-    int32_t d;
-    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(h), "v"(x));
-    return d;
-}
-
 // the SPT samples (SPT*4 bytes) this thread contributes to the FPB hops starting at first_hop
 __device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int tid, uint4& v0, uint4& v1) {
     constexpr int SPT = G4::SPT;
@@ -84,7 +65,6 @@ __device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int
         return;
     }
     if (s0 >= -a.avail) {
-#if MKID_NT_LOADS
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 p = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0));
         v0 = make_uint4(p.x, p.y, p.z, p.w);
@@ -92,10 +72,6 @@ __device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int
             const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.x + s0 + 4));
             v1 = make_uint4(q.x, q.y, q.z, q.w);
         }
-#else
-        v0 = *reinterpret_cast<const uint4*>(a.x + s0);
-        if constexpr (SPT == 8) v1 = *reinterpret_cast<const uint4*>(a.x + s0 + 4);
-#endif
         return;
     }
     const uint32_t* h = a.xhist + (s0 + a.avail + G4::HIST);
@@ -106,82 +82,16 @@ __device__ __forceinline__ void load8(const FrontArgs& a, int64_t first_hop, int
 // samples qoff..qoff+7 of a hop (qoff a multiple of 8) into the permuted hop layout: sample o at
 // (o % 8) Q + o / 8, i.e. one dword in each of the 8 planes (consecutive lanes, consecutive dwords)
 // (SPT = 4: samples qoff..qoff+3 go to planes qoff % 8 .. + 3; lanes 2k, 2k+1 share a bank, 2-way)
-#ifndef MKID_F4_PAIRRING
-#define MKID_F4_PAIRRING 1
-#endif
-// MKID_F4_PAIRRING: plane index i at 128 (i >> 7) + 2 (i & 63) + ((i >> 6) & 1) (k_front2.hip
-// ring3_idx), so the PFB reads points r, r + 1 of a lane with one ds_read_b64
-__device__ __forceinline__ int ring_idx4(int i) {
-#if MKID_F4_PAIRRING
-    return 128 * (i >> 7) + 2 * (i & 63) + ((i >> 6) & 1);
-#else
-    return i;
-#endif
-}
+// plane index i at ring3_idx(i) (paired planes), so the PFB reads points r, r + 1 of a lane with
+// one ds_read_b64
 __device__ __forceinline__ void ring_put8(uint32_t* hop, int qoff, uint4 v0, uint4 v1) {
     constexpr int Q = G4::Q;
-    uint32_t* p = hop + (qoff % 8) * Q + ring_idx4(qoff / 8);
+    uint32_t* p = hop + (qoff % 8) * Q + ring3_idx(qoff / 8);
     p[0] = v0.x; p[Q] = v0.y; p[2 * Q] = v0.z; p[3 * Q] = v0.w;
     if constexpr (G4::SPT == 8) {
         p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
     }
 }
-
-template <int BANKS>
-__device__ __forceinline__ float upd_ror8(float old, float src) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
-                                                                 __builtin_bit_cast(int, src), 0x128, 0xf,
-                                                                 BANKS, false));
-}
-
-// register bits <-> lane bits 3-5 (k_front2.hip t1_transpose)
-[[maybe_unused]] __device__ __forceinline__ void t1_transpose(float2 (&v)[8]) {
-#pragma unroll
-    for (int r0 = 0; r0 < 8; r0 += 2) {
-        const float2 a0 = v[r0], a1 = v[r0 + 1];
-        v[r0].x = upd_ror8<0xC>(a0.x, a1.x);
-        v[r0].y = upd_ror8<0xC>(a0.y, a1.y);
-        v[r0 + 1].x = upd_ror8<0x3>(a1.x, a0.x);
-        v[r0 + 1].y = upd_ror8<0x3>(a1.y, a0.y);
-    }
-    constexpr int kP16[4] = {0, 1, 4, 5};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r0 = kP16[i];
-        const auto sx = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].x),
-                                                         __builtin_bit_cast(int, v[r0 + 2].x), false, false);
-        const auto sy = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v[r0].y),
-                                                         __builtin_bit_cast(int, v[r0 + 2].y), false, false);
-        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
-        v[r0 + 2] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
-    }
-#pragma unroll
-    for (int r0 = 0; r0 < 4; ++r0) {
-        const auto sx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].x),
-                                                         __builtin_bit_cast(int, v[r0 + 4].x), false, false);
-        const auto sy = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v[r0].y),
-                                                         __builtin_bit_cast(int, v[r0 + 4].y), false, false);
-        v[r0] = make_float2(__builtin_bit_cast(float, (int)sx[0]), __builtin_bit_cast(float, (int)sy[0]));
-        v[r0 + 4] = make_float2(__builtin_bit_cast(float, (int)sx[1]), __builtin_bit_cast(float, (int)sy[1]));
-    }
-}
-
-__device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
-
-// T1 through the wave's own LDS region (k_front2.hip t1_lds): 8 + 8 conflict-free ds_*_b64
-// instead of 32 VALU cross-lane moves
-__device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) reg[72 * r + L] = v[r];
-    __builtin_amdgcn_wave_barrier();
-    const float2* rd = reg + 72 * (L >> 3) + (L & 7);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = rd[8 * r];
-    __builtin_amdgcn_wave_barrier();
-}
-#ifndef MKID_F4_T1LDS
-#define MKID_F4_T1LDS 1
-#endif
 
 }  // namespace
 
@@ -314,12 +224,11 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
             int sb = rb + sl0;
             sb -= sb >= RS ? RS : 0;
             float2 v[8];
-            [[maybe_unused]] uint32_t xo[T];   // MKID_F4_PAIRRING: the odd point's samples
+            uint32_t xo[T];   // the odd point's samples (paired planes)
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 const int hi = r >> 2;
                 uint32_t x4[T];
-#if MKID_F4_PAIRRING
                 if ((r & 1) == 0) {
 #pragma unroll
                     for (int tau = 0; tau < T; ++tau) {
@@ -333,19 +242,10 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
 #pragma unroll
                     for (int tau = 0; tau < T; ++tau) x4[tau] = xo[tau];
                 }
-#else
-                const int pos = w * G::Q + 64 * (r & 3) + L;
-#pragma unroll
-                for (int tau = 0; tau < T; ++tau) {
-                    int s = sb + 2 * tau + hi;
-                    s -= s >= RS ? RS : 0;
-                    x4[tau] = ring[s * M + pos];
-                }
-#endif
-                const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
-                const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
-                const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);
-                const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x07060302u);
+                const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermI);
+                const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermQ);
+                const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermI);
+                const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermQ);
                 int32_t ai = dot2_first(tq[r].x, i01);
                 ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
                 int32_t aq = dot2_first(tq[r].x, q01);
@@ -356,11 +256,7 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
             dft<8>(v);
 #pragma unroll
             for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], t1[64 * (k - 1)]);
-#if MKID_F4_T1LDS
             t1_lds(v, reg, L);
-#else
-            t1_transpose(v);
-#endif
             dft<8>(v);
 #pragma unroll
             for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], t2[8 * (k - 1)]);
@@ -444,15 +340,10 @@ __global__ __launch_bounds__(G4::BT, G4::BT / 256) void k_front4(FrontArgs a) {
                         const int c = tid + G::BT * q;
                         int qv = __float2int_rn(ph[q] * 8192.0f);
                         qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
-#if MKID_NT_STORES
 #ifndef MKID_XP_STAMPS
                         if (phase_run) __builtin_nontemporal_store(ph[q], phase_run + jr * C + c);
 #endif
                         __builtin_nontemporal_store((int16_t)qv, raw_run + jr * C + c);
-#else
-                        if (phase_run) (phase_run + jr * C)[c] = ph[q];
-                        (raw_run + jr * C)[c] = (int16_t)qv;
-#endif
                         if (c == a.iq_ch && a.iqtap) {
                             a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y[q].x);
                             a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y[q].y);
@@ -481,11 +372,8 @@ hipError_t launch_front4(const FrontArgs& a0, hipStream_t s) {
     // runs of up to 1024 frames (the 24-frame low-pass warm-up is 2.3 % of a full run): a full
     // 2^30-sample chunk is two rounds of workgroups over the device's CUs (-2.2 % against 1024
     // runs of 512 frames on MI355X's 256 CUs, tools/kbench.py A/B)
-#ifndef MKID_F4_BLOCKS_PER_CU
-#define MKID_F4_BLOCKS_PER_CU 2
-#endif
     const int64_t ncu = a.ncu > 0 ? a.ncu : 256;
-    int64_t fpb = a.K / ((int64_t)MKID_F4_BLOCKS_PER_CU * ncu);
+    int64_t fpb = a.K / (2 * ncu);
     fpb = fpb < 64 ? 64 : (fpb > 1024 ? 1024 : fpb);
     fpb = (fpb + G4::FPB - 1) / G4::FPB * G4::FPB;
     a.frames_per_block = fpb;

@@ -22,8 +22,7 @@
 // Arithmetic (PFB int16 dot products, radix-8 sub-FFTs, Horner combine in W_N^{bin} joined by
 // W_N^{4 bin}, DDC, transposed decimating low-pass, atan2, Fix16_13) is k_front4's, except that
 // W_N^{4 bin} is rebuilt by two squarings (a few ulp); both are held to the same parity bars.
-#include "fft_common.h"
-#include "mkid_internal.h"
+#include "front_common.h"
 
 #include <type_traits>
 
@@ -68,14 +67,6 @@ struct G5 {
     static_assert(lds_bytes <= 160 * 1024, "LDS");
 };
 
-typedef short fshort2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ fshort2_t as_s2(uint32_t v) { return __builtin_bit_cast(fshort2_t, v); }
-__device__ __forceinline__ int32_t dot2_first(uint32_t h, uint32_t x) {
-    int32_t d;
-    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(h), "v"(x));
-    return d;
-}
-
 // the 8 samples transform thread xt contributes to hop `hop` (samples 8 xt .. 8 xt + 7)
 __device__ __forceinline__ void load_hop(const FrontArgs& a, int64_t hop, int xt, uint4& v0, uint4& v1) {
     const int64_t s0 = hop * G5::M + (int64_t)xt * G5::SPT;
@@ -96,39 +87,23 @@ __device__ __forceinline__ void load_hop(const FrontArgs& a, int64_t hop, int xt
     v1 = *reinterpret_cast<const uint4*>(h + 4);
 }
 
-// hop layout: sample o at plane o % 8, plane index o / 8 stored at ring_idx(o / 8), the paired
+// hop layout: sample o at plane o % 8, plane index o / 8 stored at ring3_idx(o / 8), the paired
 // plane layout of k_front3 / k_front4 (plane entries 64 apart adjacent, so a lane's PFB points
 // r, r + 1 are one ds_read_b64)
-__device__ __forceinline__ int ring_idx(int i) { return 128 * (i >> 7) + 2 * (i & 63) + ((i >> 6) & 1); }
 __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 v1) {
     constexpr int Q = G5::Q;
-    uint32_t* p = hop + ring_idx(xt);
+    uint32_t* p = hop + ring3_idx(xt);
     p[0] = v0.x; p[Q] = v0.y; p[2 * Q] = v0.z; p[3 * Q] = v0.w;
     p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
 }
 
-__device__ __forceinline__ int yswz(int k) { return k ^ ((k >> 2) & 14); }
 // element i of a uniform float array as a 32-bit lane offset from the (SGPR) base
 __device__ __forceinline__ float ldf(const float* base, int i) {
     return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (uint32_t)i * 4u);
 }
 
-// T1 through the wave's own LDS region (k_front2.hip t1_lds)
-__device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) reg[72 * r + L] = v[r];
-    __builtin_amdgcn_wave_barrier();
-    const float2* rd = reg + 72 * (L >> 3) + (L & 7);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = rd[8 * r];
-    __builtin_amdgcn_wave_barrier();
-}
-
 // measured and dropped (DESIGN.md §5 k_front5): T1 in registers, LO one frame ahead, one Horner
 // chain, even/odd chains, unsplit Y reads, no barrier between channels, transform-wave priority
-#ifndef MKID_F5_NT_STORES
-#define MKID_F5_NT_STORES 1
-#endif
 
 // select / DDC / low-pass / phase of CPT channels c0 + cs q per thread, frame k - 1 of iteration t
 // (the centres are re-read from global memory at each output frame and the avgIQ sums kept in LDS
@@ -264,17 +239,10 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                         const uint32_t c = (uint32_t)(cb + cs * q);
                         int qv = __float2int_rn(ph[q] * 8192.0f);
                         qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
-#if MKID_F5_NT_STORES
 #ifndef MKID_XP_STAMPS
                         if (phase_run) __builtin_nontemporal_store(ph[q], reinterpret_cast<float*>(prow + c * 4u));
 #endif
                         __builtin_nontemporal_store((int16_t)qv, reinterpret_cast<int16_t*>(rrow + c * 2u));
-#else
-#ifndef MKID_XP_STAMPS
-                        if (phase_run) *reinterpret_cast<float*>(prow + c * 4u) = ph[q];
-#endif
-                        *reinterpret_cast<int16_t*>(rrow + c * 2u) = (int16_t)qv;
-#endif
                     }
                     if (iqhit) *reinterpret_cast<uint32_t*>(a.iqtap + 2 * ((k_b >> 1) + jr)) = iqv;
                 }
@@ -385,10 +353,10 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
                         const uint32_t* x4 = xr[r];
-                        const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x05040100u);
-                        const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], 0x07060302u);
-                        const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x05040100u);
-                        const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], 0x07060302u);
+                        const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermI);
+                        const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermQ);
+                        const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermI);
+                        const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermQ);
                         int32_t ai = dot2_first(tq[s][r].x, i01);
                         ai = __builtin_amdgcn_sdot2(as_s2(tq[s][r].y), as_s2(i23), ai, false);
                         int32_t aq = dot2_first(tq[s][r].x, q01);

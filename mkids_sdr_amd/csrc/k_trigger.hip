@@ -164,7 +164,7 @@ struct Stepper<MKID_BASE_SVF, true> {
     __device__ Stepper(const TrigState& s, const TrigCfg& k, int32_t f0)
         : fs(to_fast_svf(s)), q(fast_cfg(k)), kf(k.kf), kq(k.kq) {
         if (!s.binit) {   // trig_update's baseline initialisation on the first sample
-            fs.low = (int64_t)f0 << 16;
+            fs.low = (int64_t)f0 * 65536;
             fs.band = 0;
         }
     }

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "mkid_internal.h"
+#include "mkid_plan.h"
 
 using namespace mkid;
 
@@ -32,44 +33,10 @@ struct KTime {
     hipEvent_t a, b;
 };
 
-// Speculative trigger segmentation (k_trigger.hip): segments of at least kSegL phase samples,
-// each speculating from kSegW samples of warm-up. The EMA baseline (alpha 41/512) forgets its
-// start in ~10^2 samples on noisy phase (SVF: see kSvfW below). A long call uses
-// longer segments so that the (channel, segment) waves fit the GPU's resident wave slots in one
-// round (less warm-up per sample, no tail round).
-#ifndef MKID_SEG_L
-#define MKID_SEG_L 2048
-#endif
-#ifndef MKID_SEG_W
-#define MKID_SEG_W 520
-#endif
-constexpr int64_t kSegL = MKID_SEG_L;
-constexpr int64_t kSegW = MKID_SEG_W;  // multiple of the 26-sample matched-filter ring
-static_assert(kSegW % kFirTaps == 0 && kSegL >= kSegW + kRawHist, "segment geometry");
-int64_t seg_capacity(int64_t L, int dead) { return L / (dead + 3) + 2; }
-
-// SVF baseline (Chamberlin 2-pole, Kf 82 / Kq 93623 Fix18_16): two integer trajectories started
-// from different states coincide only after ~10^4 samples (the difference decays with the
-// filter's ~1100-sample time constant, then random-walks through the shift roundings to zero:
-// median 1.5e4, 99th percentile 2.9e4, max 3.9e4 over 1024 simulated noisy channels; on the
-// bench stream a 49k-sample warm-up still missed 0.3 % of segments, 98k about 1 in 30000,
-// DESIGN.md §5), so SVF segments speculate from kSvfW samples of warm-up and are at least
-// kSvfLmin long; a segment closer than kSvfW to the sub-chunk start warms up from the carried
-// (exact) state at row 0. Segment lengths are multiples of 26 so that every warm-up start keeps
-// the filter ring aligned. The per-lane walk is latency bound: one segment per two SIMD lanes
-// (svf_lanes) balanced against the warm-up redundancy measured best (tools/svf_sweep.sh).
-#ifndef MKID_SVF_W
-#define MKID_SVF_W (26 * 3780)
-#endif
-constexpr int64_t kSvfW = MKID_SVF_W;
-constexpr int64_t kSvfLmin = 26 * 158;
-static_assert(kSvfW % kFirTaps == 0, "SVF warm-up geometry");
-
-// segment length for J rows: >= kSegL, and (C/64) * ceil(J/L) waves <= the resident slots
-int64_t seg_length(int64_t J, int C, int64_t wave_slots) {
-    const int64_t nt = std::max<int64_t>(1, wave_slots * 64 / C);
-    return std::max<int64_t>(kSegL, (J + nt - 1) / nt);
-}
+using plan::kSegL;
+using plan::kSvfW;
+using plan::seg_capacity;
+using plan::SubPlan;
 
 }  // namespace
 
@@ -126,6 +93,7 @@ struct mkid_ctx {
     int64_t nseg_max = 0, slot_cap = 0, scratch_cap = 0, trig_slots = 0;
     int64_t svf_lanes = 65536, svf_w = kSvfW;  // SVF segmentation (plan_sub)
     int64_t nsub_max = 0;    // sub-chunks per call (ceil(max_chunk / G))
+    plan::Workspace ws;      // what the context was sized for (plan::size_workspace)
     int64_t* d_counts = nullptr;  // [2] used by the host-pointer API
     int64_t last_J = 0;     // phase rows of the last call
     int64_t last_subJ = 0;  // rows of its last sub-chunk (held in d_raw)
@@ -271,44 +239,7 @@ struct DevBufs {
     }
 };
 
-// K1 taps as the device applies them (include/mkidgpu.h, mkid_set_pfb): h_q = rint(h 2^S) int16
-// with the largest S such that every point's four |h_q| sum to <= 65535 and every |h_q| <= 32767
-// (so the fused kernel's int16 dot products never overflow int32 on int16 samples).
-static int quantize_pfb(const float* h, int T, int N, std::vector<int16_t>& hq) {
-    double ms = 0.0, ma = 0.0;
-    for (int p = 0; p < N; ++p) {
-        double sp = 0.0;
-        for (int t = 0; t < T; ++t) {
-            const double a = std::fabs((double)h[t * N + p]);
-            sp += a;
-            ma = std::max(ma, a);
-        }
-        ms = std::max(ms, sp);
-    }
-    int S = 0;
-    if (ms > 0.0) {
-        S = -64;
-        while (S < 64 && std::ldexp(ms, S + 1) <= 65535.0 && std::ldexp(ma, S + 1) <= 32767.0) ++S;
-    }
-    hq.resize((size_t)T * N);
-    // rounding can push a point's sum of |h_q| past 65535 (and a dot product of full-scale
-    // samples past INT32_MAX): step S down until the ROUNDED taps obey both bounds
-    for (;; --S) {
-        for (size_t i = 0; i < hq.size(); ++i) hq[i] = (int16_t)std::rint(std::ldexp((double)h[i], S));
-        bool ok = true;
-        for (int p = 0; p < N && ok; ++p) {
-            int64_t sp = 0;
-            for (int t = 0; t < T; ++t) {
-                const double r = std::rint(std::ldexp((double)h[t * N + p], S));
-                if (std::fabs(r) > 32767.0) ok = false;
-                sp += (int64_t)std::fabs(r);
-            }
-            if (sp > 65535) ok = false;
-        }
-        if (ok || S <= -64) break;
-    }
-    return S;
-}
+using plan::quantize_pfb;
 
 static int upload_lo_folded(mkid_ctx* c);
 static int upload_slot_order(mkid_ctx* c);
@@ -365,43 +296,36 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
         const char* so = getenv("MKID_SLOT_ORDER");
         c->slot_order_on = !(so && atoi(so) == 0);
     }
-    // split front end: a large call is cut into 4 sub-chunks so the channeliser (stream A) of
-    // sub-chunk i+1 overlaps the low-pass/trigger (stream B) of sub-chunk i
-    int64_t G = cfg->max_chunk;
-    if (!c->fused && G >= (int64_t)512 * N) {
-        G = cfg->max_chunk / 4;
-        G -= G % N;
-    }
-    c->G = G;
-    c->Kmax = G / c->M;
-    c->Jmax = G / N;
-    c->nsub_max = (cfg->max_chunk + G - 1) / G;
-    // Packet capacities are hard bounds: an event needs >= dead_time + 3 phase samples (trigger,
-    // peak, dead time, re-arm), so no per-channel/segment overflow can occur.
-    const int64_t cap_bound = c->Jmax / (cfg->dead_time + 3) + 2;  // whole call, one segment
-    c->capc = (int)std::min<int64_t>(cfg->max_events_per_ch > 0 ? cfg->max_events_per_ch : cap_bound, INT_MAX / 2);
-    c->trig_slots = trigger_wave_slots(device);
+    int64_t trig_slots = trigger_wave_slots(device);
     // tuning/test knob: pretend the GPU holds this many trigger waves (forces longer segments)
-    if (const char* ev = getenv("MKID_TRIG_WAVE_SLOTS")) c->trig_slots = std::max<int64_t>(1, atoll(ev));
+    if (const char* ev = getenv("MKID_TRIG_WAVE_SLOTS")) trig_slots = std::max<int64_t>(1, atoll(ev));
+    int64_t svf_lanes = 0, svf_w = kSvfW;
     {   // SVF segments: one per two SIMD lanes (4 SIMDs x 64 lanes per CU); test/tuning knobs
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
             ncu = 256;
         c->ncu = ncu;
-        c->svf_lanes = (int64_t)ncu * 128;
-        if (const char* ev = getenv("MKID_SVF_LANES")) c->svf_lanes = std::max<int64_t>(1, atoll(ev));
+        svf_lanes = (int64_t)ncu * 128;
+        if (const char* ev = getenv("MKID_SVF_LANES")) svf_lanes = std::max<int64_t>(1, atoll(ev));
         if (const char* ev = getenv("MKID_SVF_WARMUP"))
-            c->svf_w = std::max<int64_t>(1, atoll(ev) / kFirTaps) * kFirTaps;
+            svf_w = std::max<int64_t>(1, atoll(ev) / kFirTaps) * kFirTaps;
     }
-    const int64_t Lmax = seg_length(c->Jmax, C, c->trig_slots);
-    // for J <= Jmax: L(J) <= Lmax and ceil(J / L(J)) <= max(slots * 64 / C, ceil(Jmax / kSegL))
-    c->nseg_max = std::max<int64_t>(std::max<int64_t>(1, c->trig_slots * 64 / C), (c->Jmax + kSegL - 1) / kSegL);
-    const int64_t capseg = seg_capacity(Lmax, cfg->dead_time);
-    // one [C][sum of the sub-chunks' segments][capseg] table per call (single compaction)
-    c->slot_cap = (int64_t)C * c->nsub_max * std::max<int64_t>(c->nseg_max * capseg, c->capc);
-    // the fix-up re-runs one segment per channel into [C][capseg]: any plan's capseg, including an
-    // SVF segment as long as the whole call (plan_sub), whatever max_events_per_ch says
-    c->scratch_cap = std::max<int64_t>(std::max<int64_t>(capseg, c->capc), seg_capacity(c->Jmax, cfg->dead_time));
+    if (const char* msg = plan::size_workspace(*cfg, c->fused, trig_slots, svf_lanes, svf_w, c->ws)) {
+        g_err = msg;
+        delete c;
+        return MKID_E_ARG;
+    }
+    c->G = c->ws.G;
+    c->Kmax = c->ws.Kmax;
+    c->Jmax = c->ws.Jmax;
+    c->nsub_max = c->ws.nsub_max;
+    c->capc = (int)c->ws.capc;
+    c->trig_slots = c->ws.trig_slots;
+    c->svf_lanes = c->ws.svf_lanes;
+    c->svf_w = c->ws.svf_w;
+    c->nseg_max = c->ws.nseg_max;
+    c->slot_cap = c->ws.slot_cap;
+    c->scratch_cap = c->ws.scratch_cap;
     c->H = c->fused ? front_hist_samples(N) : (int64_t)c->T * N - c->M;
     const int64_t H = c->H;
     auto fail = [&](hipError_t e, const char* what) {
@@ -573,67 +497,8 @@ int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
     return upload_lo_folded(c);
 }
 
-// The select threads of k_front3 (C = 1024) and k_front4 (C = 2048) read Y at entry
-// yswz(bin & 511) of each sub-FFT region (regions and frames are 0 mod 32 entries apart), so a
-// channel's LDS bank pair is that entry mod 32; a ds_read_b64 costs one LDS cycle per distinct
-// address on the busiest pair of each 32-lane half (MI355X_MICROARCH.md §LDS). Slot
-// st + (C/2) q (st = 64 w + 32 h + l) is read by lane 32 h + l of wave w in instruction q; wave w
-// owns channels 128 w .. 128 w + 127 and reads them in four groups of 32. In channel order random
-// bins cost ~3.4 cycles per group. Greedy per wave: its channels by pair-class size, each into the
-// group whose cost rises least, then whose new cost is lowest, then the emptiest: ~1.9 cycles per
-// group (tools/lds_assign.py holds the same algorithm and its model).
-// k_front4 (C = 2048) has the same read pattern but loses with the order (+0.5 % with plain stores,
-// +2.6 % with its non-temporal ones: profiles/r03_h_kbench_f4_slot_order.json), so only k_front3
-// takes it; mkid_slot_order still reports the C = 2048 order for the model and tests.
-static void slot_order(const std::vector<int32_t>& bins, int C, std::vector<int16_t>& out) {
-    out.resize(C);
-    for (int i = 0; i < C; ++i) out[i] = (int16_t)i;
-    if (C != 1024 && C != 2048) return;
-    constexpr int B = 128, NG = 4, GS = 32;
-    auto yoff = [](int b) { const int k = b & 511; return k ^ ((k >> 2) & 14); };
-    for (int w = 0; w < C / B; ++w) {
-        int cnt[32] = {0};
-        int yo[B];
-        for (int i = 0; i < B; ++i) {
-            yo[i] = yoff(bins[B * w + i]);
-            ++cnt[yo[i] & 31];
-        }
-        std::vector<int> order(B);
-        for (int i = 0; i < B; ++i) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-            const int ka = yo[a] & 31, kb = yo[b] & 31;
-            if (cnt[ka] != cnt[kb]) return cnt[ka] > cnt[kb];
-            if (ka != kb) return ka < kb;
-            return yo[a] < yo[b];
-        });
-        int size[NG] = {0}, gmax[NG] = {0}, mult[NG][32] = {{0}};
-        std::vector<int> seen[NG];
-        int member[NG][GS];
-        for (int i : order) {
-            const int k = yo[i] & 31;
-            int bg = -1, bk0 = 0, bk1 = 0, bk2 = 0;
-            bool bsame = false;
-            for (int g = 0; g < NG; ++g) {
-                if (size[g] >= GS) continue;
-                const bool same = std::find(seen[g].begin(), seen[g].end(), yo[i]) != seen[g].end();
-                const int m = mult[g][k] + (same ? 0 : 1);
-                const int nm = std::max(gmax[g], m);
-                const int k0 = nm - gmax[g], k1 = nm, k2 = size[g];
-                if (bg < 0 || k0 < bk0 || (k0 == bk0 && (k1 < bk1 || (k1 == bk1 && k2 < bk2)))) {
-                    bg = g; bk0 = k0; bk1 = k1; bk2 = k2; bsame = same;
-                }
-            }
-            member[bg][size[bg]++] = B * w + i;
-            if (!bsame) {
-                seen[bg].push_back(yo[i]);
-                ++mult[bg][k];
-            }
-            gmax[bg] = std::max(gmax[bg], mult[bg][k]);
-        }
-        for (int g = 0; g < NG; ++g)
-            for (int l = 0; l < GS; ++l) out[64 * w + 32 * (g & 1) + l + (C / 2) * (g >> 1)] = (int16_t)member[g][l];
-    }
-}
+// k_front3 select-slot order: plan::slot_order (mkid_plan.cpp)
+using plan::slot_order;
 
 static int upload_slot_order(mkid_ctx* c) {
     std::vector<int16_t> so;
@@ -735,61 +600,10 @@ int mkid_reset_stream(mkid_ctx* c) {
     return MKID_OK;
 }
 
-// Trigger geometry of one sub-chunk of J phase rows: segment length L, warm-up W, nseg segments
-// and the per-segment packet capacity.
-struct SubPlan {
-    int64_t J;
-    int32_t L, W, nseg, capseg;
-};
-
-static SubPlan plan_sub(const mkid_ctx* c, int64_t J) {
-    if (c->mode == MKID_BASE_SVF) {
-        // svf_lanes segments over all channels (the per-lane walk is latency bound), each
-        // >= kSvfLmin rows; short sub-chunks run as one exact segment
-        const int64_t want = std::max<int64_t>(1, c->svf_lanes / c->C);
-        int64_t nseg = std::min<int64_t>(std::min<int64_t>(want, J / kSvfLmin), c->nseg_max);
-        SubPlan p;
-        p.J = J;
-        p.W = 0;
-        p.L = (int32_t)J;
-        p.nseg = 1;
-        if (nseg > 1 && J > 2 * kSvfLmin) {
-            int64_t L = (J + nseg - 1) / nseg;
-            L = (L + kFirTaps - 1) / kFirTaps * kFirTaps;
-            p.L = (int32_t)L;
-            p.W = (int32_t)c->svf_w;
-            p.nseg = (int32_t)((J + L - 1) / L);
-        }
-        p.capseg = (int32_t)seg_capacity(p.L, c->cfg.dead_time);
-        return p;
-    }
-    const bool serial = J <= kSegL;
-    // segment starts at multiples of 26 (the trigger's window ring is group-aligned)
-    const int64_t Ls = serial ? J : (seg_length(J, c->C, c->trig_slots) + kFirTaps - 1) / kFirTaps * kFirTaps;
-    SubPlan p;
-    p.J = J;
-    p.L = (int32_t)Ls;
-    p.W = serial ? 0 : (int32_t)kSegW;
-    p.nseg = (int32_t)((J + Ls - 1) / Ls);
-    p.capseg = (int32_t)seg_capacity(Ls, c->cfg.dead_time);
-    return p;
-}
-
-// The sub-chunk plans of a call of n samples and the call's slot-table geometry: stride = total
-// segments per channel, capseg = the largest per-segment capacity (the table is uniform).
-static int plan_call(mkid_ctx* c, int64_t n, int64_t G, std::vector<SubPlan>& subs, int32_t& stride,
-                     int32_t& capseg) {
-    subs.clear();
-    stride = 0;
-    capseg = 1;
-    for (int64_t off = 0; off < n; off += G) {
-        subs.push_back(plan_sub(c, std::min<int64_t>(G, n - off) / c->N));
-        stride += subs.back().nseg;
-        capseg = std::max(capseg, subs.back().capseg);
-        if (subs.back().nseg > c->nseg_max) FAIL(c, MKID_E_ARG, "trigger plan exceeds the segment tables");
-    }
-    if ((int64_t)c->C * stride * capseg > c->slot_cap) FAIL(c, MKID_E_ARG, "trigger plan exceeds the packet slot table");
-    if (capseg > c->scratch_cap) FAIL(c, MKID_E_ARG, "trigger plan exceeds the fix-up scratch");
+// The call's trigger plan (plan::plan_call, mkid_plan.cpp) within the context's workspace.
+static int plan_call(mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, int32_t& stride, int32_t& capseg) {
+    if (const char* msg = plan::plan_call(c->ws, c->C, c->N, c->mode, c->cfg.dead_time, n, subs, stride, capseg))
+        FAIL(c, MKID_E_ARG, msg);
     return MKID_OK;
 }
 
@@ -837,7 +651,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
     {
-        int r = plan_call(c, n, G, subs, stride, capseg);
+        int r = plan_call(c, n, subs, stride, capseg);
         if (r) return r;
     }
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, A));
@@ -895,25 +709,16 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     return MKID_OK;
 }
 
-int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
-                        int64_t cap, int64_t* d_counts) {
-    if (!c || !d_iq || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
-    if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
-    // the workspace (raw rows, IQ tap, slot table) is sized for max_chunk samples per call
-    if (n > c->cfg.max_chunk) FAIL(c, MKID_E_ARG, "nsamples exceeds cfg.max_chunk");
-    if (((uintptr_t)d_iq & 15) != 0) FAIL(c, MKID_E_ARG, "d_iq must be 16-byte aligned");
-    if (c->stream_kind == 2)
-        FAIL(c, MKID_E_STATE, "the context carries a phase-row stream (mkid_trigger_phase); mkid_reset_stream first");
-    c->stream_kind = 1;
-    HIPCHK(c, hipSetDevice(c->device));
-    if (c->fused) return process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts);
+// Split front end (channeliser on stream A, low-pass / trigger / compaction on stream B).
+static int process_split(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
+                         int64_t cap, int64_t* d_counts) {
     const int C = c->C, N = c->N, M = c->M;
     const int64_t H = c->H;
     hipStream_t A = c->stream, B = c->sB;
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
     {
-        int r = plan_call(c, n, c->G, subs, stride, capseg);
+        int r = plan_call(c, n, subs, stride, capseg);
         if (r) return r;
     }
     // B joins A's order (inputs written by earlier work on A, previous calls) ...
@@ -987,6 +792,24 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     return MKID_OK;
 }
 
+int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
+                        int64_t cap, int64_t* d_counts) {
+    if (!c || !d_iq || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
+    if (n <= 0 || n % c->N != 0) FAIL(c, MKID_E_ARG, "nsamples must be a positive multiple of N");
+    // the workspace (raw rows, IQ tap, slot table) is sized for max_chunk samples per call
+    if (n > c->cfg.max_chunk) FAIL(c, MKID_E_ARG, "nsamples exceeds cfg.max_chunk");
+    if (((uintptr_t)d_iq & 15) != 0) FAIL(c, MKID_E_ARG, "d_iq must be 16-byte aligned");
+    if (c->stream_kind == 2)
+        FAIL(c, MKID_E_STATE, "the context carries a phase-row stream (mkid_trigger_phase); mkid_reset_stream first");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int r = c->fused ? process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts)
+                           : process_split(c, d_iq, n, d_phase, d_events, cap, d_counts);
+    // the context carries an ADC stream only once a call has been enqueued (a call that failed
+    // before, e.g. in planning, leaves the stream kind as it was)
+    if (r == MKID_OK) c->stream_kind = 1;
+    return r;
+}
+
 int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t* d_events, int64_t cap,
                        int64_t* d_counts) {
     if (!c || !d_raw || !d_counts || (cap > 0 && !d_events)) return MKID_E_ARG;
@@ -994,13 +817,12 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
     if (((uintptr_t)d_raw & 3) != 0) FAIL(c, MKID_E_ARG, "d_raw must be 4-byte aligned");
     if (c->stream_kind == 1)
         FAIL(c, MKID_E_STATE, "the context carries an ADC stream (mkid_process); mkid_reset_stream first");
-    c->stream_kind = 2;
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = c->stream;
     std::vector<SubPlan> subs;
     int32_t stride = 0, capseg = 0;
     {
-        int r = plan_call(c, rows * c->N, c->G, subs, stride, capseg);
+        int r = plan_call(c, rows * c->N, subs, stride, capseg);
         if (r) return r;
     }
     HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
@@ -1013,7 +835,9 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
         r0 += sp.J;
         c->j0 += sp.J;
     }
-    return compact_call(c, stride, capseg, d_events, cap, d_counts, s);
+    const int r = compact_call(c, stride, capseg, d_events, cap, d_counts, s);
+    if (r == MKID_OK) c->stream_kind = 2;   // as mkid_process_device: only once enqueued
+    return r;
 }
 
 int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, uint64_t* events_out, int64_t cap,
@@ -1053,10 +877,7 @@ int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, ui
         written += take;
     }
     *nevents = produced;
-    if (n > chunk && written > 1)   // chunks were compacted separately: merge to channel-major
-        std::stable_sort(events_out, events_out + written, [](uint64_t a, uint64_t b) {
-            return (a >> MKID_PKT_CH_SHIFT) < (b >> MKID_PKT_CH_SHIFT);
-        });
+    if (n > chunk) plan::merge_channel_major(events_out, written);   // chunks were compacted separately
     if (produced > written) FAIL(c, MKID_E_OVERFLOW, "event capacity exceeded; events dropped");
     return MKID_OK;
 }
@@ -1332,16 +1153,7 @@ int mkid_synth_adc(mkid_ctx* c, int16_t* d_out, int64_t n, int64_t n0, const int
 
 int mkid_pack_reference(const uint64_t* wide, int64_t n, uint64_t* out) {
     if ((!wide || !out) && n > 0) return MKID_E_ARG;
-    for (int64_t i = 0; i < n; ++i) {
-        const uint64_t w = wide[i];
-        const uint64_t ch = (w >> MKID_PKT_CH_SHIFT) & 0xFFF;
-        if (ch >= 255) return MKID_E_ARG;  // 8-bit channel field, 255 = end-of-second marker
-        const uint64_t pk = (w >> MKID_PKT_PEAK_SHIFT) & 0xFFF, bs = (w >> MKID_PKT_BASE_SHIFT) & 0xFFF;
-        const uint64_t p1 = (uint64_t)std::min<int64_t>(4095, std::max<int64_t>(0, (int64_t)pk - (int64_t)bs + 2048));
-        const uint64_t ts = w & 0xFFFFF;
-        out[i] = (ch << 56) | (pk << 44) | (p1 << 32) | (bs << 20) | ts;
-    }
-    return MKID_OK;
+    return plan::pack_reference(wide, n, out) == 0 ? MKID_OK : MKID_E_ARG;
 }
 
 }  // extern "C"

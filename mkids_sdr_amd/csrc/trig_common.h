@@ -48,7 +48,7 @@ __device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigC
     // the state DEAD for kHoldOff samples with no baseline, oracle/trigger.c HOLDOFF)
     if (!s.binit && s.st != ST_DEAD) {
         s.B = (k.mode == MKID_BASE_NONE) ? 0 : f;
-        s.low = (int64_t)f << 16;
+        s.low = (int64_t)f * 65536;
         s.band = 0;
         s.binit = 1;
     }
@@ -58,7 +58,7 @@ __device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigC
     if (k.mode == MKID_BASE_EMA && s.binit) {
         s.B += gate ? ((k.alpha * e) >> 9) : 0;
     } else if (k.mode == MKID_BASE_SVF && gate && s.binit) {
-        const int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)k.kq * s.band) >> 16);
+        const int64_t high = ((int64_t)f * 65536) - s.low - (((int64_t)k.kq * s.band) >> 16);
         s.band += ((int64_t)k.kf * high) >> 16;
         s.low += ((int64_t)k.kf * s.band) >> 16;
     }
@@ -168,7 +168,7 @@ __device__ __forceinline__ int64_t mul_u32_i64(uint32_t a, int64_t b) {
 __device__ __forceinline__ void base_update_svf(FastSvf& s, int32_t f, const FastCfg& k, int32_t kf, int32_t kq) {
     const int32_t e = f - (int32_t)(s.low >> 16);
     const bool gate = (uint32_t)e + k.goff < k.glim;
-    const int64_t high = ((int64_t)f << 16) - s.low - (mul_u32_i64((uint32_t)kq, s.band) >> 16);
+    const int64_t high = ((int64_t)f * 65536) - s.low - (mul_u32_i64((uint32_t)kq, s.band) >> 16);
     const int64_t band = s.band + (mul_u32_i64((uint32_t)kf, high) >> 16);
     const int64_t low = s.low + (mul_u32_i64((uint32_t)kf, band) >> 16);
     s.band = gate ? band : s.band;
@@ -186,7 +186,7 @@ __device__ __forceinline__ bool trig_update_svf(FastSvf& s, int32_t f, const Fas
         // into blocks the register allocator spills across)
         const bool gate = (uint32_t)e + k.goff < k.glim;
         // kf, kq are Fix18_16 in 0..2^18-1 (mkid_set_baseline checks)
-        const int64_t high = ((int64_t)f << 16) - s.low - (mul_u32_i64((uint32_t)kq, s.band) >> 16);
+        const int64_t high = ((int64_t)f * 65536) - s.low - (mul_u32_i64((uint32_t)kq, s.band) >> 16);
         const int64_t band = s.band + (mul_u32_i64((uint32_t)kf, high) >> 16);
         const int64_t low = s.low + (mul_u32_i64((uint32_t)kf, band) >> 16);
         s.band = gate ? band : s.band;

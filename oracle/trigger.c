@@ -75,7 +75,7 @@ int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* 
             int32_t f = clamp16(acc >> 11);
             if (!s.binit && s.st != ST_DEAD) { /* first sample after the hold-off */
                 s.B = (mode == 0) ? 0 : f;
-                s.low = (int64_t)f << 16;
+                s.low = (int64_t)f * 65536;
                 s.band = 0;
                 s.binit = 1;
             }
@@ -85,7 +85,7 @@ int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* 
             if (s.binit && mode == 1 && gate) {
                 s.B += (alpha * e) >> 9;
             } else if (s.binit && mode == 2 && gate) {
-                int64_t high = ((int64_t)f << 16) - s.low - (((int64_t)kq * s.band) >> 16);
+                int64_t high = ((int64_t)f * 65536) - s.low - (((int64_t)kq * s.band) >> 16);
                 s.band += ((int64_t)kf * high) >> 16;
                 s.low += ((int64_t)kf * s.band) >> 16;
             }

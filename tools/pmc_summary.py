@@ -5,14 +5,20 @@
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3 KiB; HBM bytes per launch = 2 x FETCH_SIZE (gfx950 counts
 half of a wide coalesced read, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both x 1024. The PMC passes
-run bench.py on a 2^28-sample step; bench.py scales `traffic` to its own launch size.
+run bench.py on one step of the workload given to tools/profile.sh (2^30 samples at configs 3 and 5);
+the config and the samples per launch are read from the run's own bench line (prof_TAG/kt.log,
+tools/prof_meta.py) and filed under that config; bench.py scales `traffic` to its own launch size.
 """
 import argparse
 import csv
 import glob
 import json
 import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from prof_meta import resolve  # noqa: E402
 
 KEEP = ('k_front', 'k_channelize', 'k_lpf_phase', 'k_trig_spec', 'k_trig_fix', 'k_tile_sums', 'k_tile_scan',
         'k_gather_events')
@@ -55,11 +61,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('dir')
     ap.add_argument('--json')
-    ap.add_argument('--samples-log2', type=int, default=28, help='ADC samples per launch in the PMC run')
-    ap.add_argument('--config', type=int, default=3, help='bench config the run measured (json key)')
+    ap.add_argument('--summary-out', help='also write the per-kernel lines to this file (profiles/...)')
+    ap.add_argument('--samples-log2', type=int, default=None,
+                    help='ADC samples per launch (only for runs without a bench line; else checked)')
+    ap.add_argument('--config', type=int, default=None,
+                    help='bench config (only for runs without a bench line; else checked)')
     a = ap.parse_args()
+    a.config, samples = resolve(a.dir.rstrip('/'), a.config, None if a.samples_log2 is None else 1 << a.samples_log2)
+    a.samples_log2 = samples.bit_length() - 1
+    assert 1 << a.samples_log2 == samples
     s = read(a.dir)
     res = {}
+    lines = []
     for k, c in sorted(s.items()):
         line = {n: round(v, 1) for n, v in sorted(c.items())}
         if 'FETCH_SIZE' in c and 'WRITE_SIZE' in c:
@@ -73,11 +86,16 @@ def main():
                 if n in c:
                     line[n + '/WAVE_CYCLES'] = round(c[n] / w, 3)
         res[k] = line
-        print(k, json.dumps(line))
+        lines.append('%s %s' % (k, json.dumps(line)))
+        print(lines[-1])
+    if a.summary_out:
+        with open(a.summary_out, 'w') as f:
+            f.write('\n'.join(lines) + '\n')
     if a.json:
         out = {k: {'hbm_bytes_per_launch': v.get('hbm_bytes_per_launch'),
                    'hbm_bytes_per_sample': v.get('hbm_bytes_per_sample'),
-                   'pmc_samples': 1 << a.samples_log2, 'source': a.dir}
+                   'pmc_samples': 1 << a.samples_log2, 'source': a.dir.rstrip('/'),
+                   'bench_config': a.config, 'summary': a.summary_out}
                for k, v in res.items() if 'hbm_bytes_per_launch' in v}
         rec = json.load(open(a.json)) if os.path.exists(a.json) else {}
         rec = {k: v for k, v in rec.items() if k.startswith('config')}   # config-keyed layout

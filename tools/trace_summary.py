@@ -11,15 +11,24 @@ import argparse
 import csv
 import json
 import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from prof_meta import resolve_config  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('csv')
     ap.add_argument('--json', help='update this file: {"config<N>": {kernel: avg ms of its largest-grid launches}}')
-    ap.add_argument('--config', type=int, default=3)
+    ap.add_argument('--config', type=int, default=None,
+                    help='bench config (only for traces without a bench line next to them; else checked)')
     a = ap.parse_args()
+    # prof_TAG/kt/run_kernel_trace.csv: the bench line is prof_TAG/kt.log
+    prof_dir = os.path.dirname(os.path.dirname(os.path.abspath(a.csv)))
+    if a.json:
+        a.config = resolve_config(prof_dir, a.config)
     rows = list(csv.DictReader(open(a.csv)))
     g = defaultdict(list)
     for r in rows:
@@ -46,6 +55,7 @@ def main():
         rec = json.load(open(a.json)) if os.path.exists(a.json) else {}
         rec['config%d' % a.config] = {k: round(v[1], 4) for k, v in best.items()}
         rec['config%d' % a.config]['source'] = a.csv
+        rec['config%d' % a.config]['bench_config'] = a.config
         json.dump(rec, open(a.json, 'w'), indent=1)
 
 

@@ -45,26 +45,6 @@ __device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Raw buffer access (vector memory instructions, buffer_load / buffer_store ... offen): a uniform
-// base in an SGPR descriptor, a uniform byte offset in an SGPR (soffset) and a per-lane 32-bit byte
-// offset (voffset) that stays loop-invariant in a VGPR, so a row-by-row walk issues no per-lane
-// address arithmetic at all (a flat / global access needs a 64-bit VGPR address per access).
-// Descriptor word 3 for gfx9 (ck_tile's CK_TILE_BUFFER_RESOURCE_3RD_DWORD), full 32-bit range.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)0xffffffff, 0x00020000);
-}
-__device__ __forceinline__ float2 buf_ld_f2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    // the builtin returns a vector_size(8) unsigned int pair: reinterpret it whole (a conversion to
-    // an ext_vector_type splats its first element)
-    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
-}
-__device__ __forceinline__ void buf_st_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, 0);
-}
-__device__ __forceinline__ void buf_st_i16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, int16_t v) {
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, r, (int)voff, (int)soff, 0);
-}
-
 // 16 bytes (4 samples) at sample tid * 4 of the hops starting at first_hop (hop = M samples):
 // non-temporal loads from the chunk (every ADC byte is read once), the call's history (the last
 // front_hist_samples of the previous call) before it, zeros past the chunk's end

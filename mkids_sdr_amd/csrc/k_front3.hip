@@ -5,26 +5,16 @@
 namespace mkid {
 
 namespace {
-// Pair ring (round 4). The PFB of point p, frame k is sum_tau h_tau x[hop k - 7 + hi + 2 tau][o]
-// (hi = p / M, o = p mod M), evaluated as two v_dot2_i32_i16 per component over 16-bit pairs
-// (x[s], x[s + 2]) of the same offset two hops apart. Those pairs used to be built per point per
-// frame with 4 v_perm from the interleaved I/Q words; every sample is read by 8 (frame, point)
-// PFB evaluations, so the ring now stores the pairs themselves, built once at refill: pair-hop
-// P(s)[o] = (I pair, Q pair) = ({I x[s][o], I x[s+2][o]}, {Q x[s][o], Q x[s+2][o]}), 8 bytes.
-// The refill thread that loads hop s + 2 at offsets o..o+3 loaded hop s at the same offsets one
-// iteration earlier and kept it in registers (`prev`), so a pair costs one v_perm per component
-// (2 per sample, against 8 per sample before).
-// Layout of a pair-hop (1024 samples, 8 KiB): plane u = o % 4 (256 entries of 8 B), plane index
-// i = o / 4 at entry ring3_idx(i), so a lane's points j, j + 1 (i = 64 j + L, j even) are one
-// conflict-free ds_read_b128. Refill thread g' (0..255 of its hop) owns plane index
-// i = 128 (g' >> 7) + ((g' >> 1) & 63) + 64 (g' & 1), whose entry is ring3_idx(i) = g': each of its
-// four ds_write_b64 (one per plane) is consecutive across lanes, conflict-free.
-__device__ __forceinline__ int pair_owner_index(int g) { return 128 * (g >> 7) + ((g >> 1) & 63) + 64 * (g & 1); }
-__device__ __forceinline__ void pair_put(uint2* phop, int g, uint4 prev, uint4 cur) {
-    phop[g] = make_uint2(__builtin_amdgcn_perm(cur.x, prev.x, kPermI), __builtin_amdgcn_perm(cur.x, prev.x, kPermQ));
-    phop[256 + g] = make_uint2(__builtin_amdgcn_perm(cur.y, prev.y, kPermI), __builtin_amdgcn_perm(cur.y, prev.y, kPermQ));
-    phop[512 + g] = make_uint2(__builtin_amdgcn_perm(cur.z, prev.z, kPermI), __builtin_amdgcn_perm(cur.z, prev.z, kPermQ));
-    phop[768 + g] = make_uint2(__builtin_amdgcn_perm(cur.w, prev.w, kPermI), __builtin_amdgcn_perm(cur.w, prev.w, kPermQ));
+// k_front3 ring plane layout (NW = 4, Q = 256 samples per plane): samples qoff..qoff+3 of a hop go
+// to planes 0..3 at plane index qoff / 4, paired (ring3_idx). The refill's ds_write_b32 become
+// 2-way bank conflicts, which cost no extra cycles for ds_write_b32 (MI355X_MICROARCH.md §LDS).
+__device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
+    constexpr int Q = 256;
+    const int a = ring3_idx(qoff / 4);
+    hop[a] = v.x;
+    hop[Q + a] = v.y;
+    hop[2 * Q + a] = v.z;
+    hop[3 * Q + a] = v.w;
 }
 }  // namespace
 // In k_front2 every wave runs the FFT phase, then every wave runs the select phase, with a
@@ -35,34 +25,35 @@ __device__ __forceinline__ void pair_put(uint2* phop, int g, uint4 prev, uint4 c
 // phase (two channels per thread), one iteration behind, on a double-buffered Y: each SIMD holds
 // two FFT and two select waves whose LDS waits and VALU bursts interleave, one barrier per
 // iteration.
-//   ring  RS = 9 pair-hops P(s) (above): iteration t (frames k, k+1) reads P(k-7) .. P(k-1) while
-//         its FFT waves write P(k), P(k+1) (from hops k+2, k+3, prefetched at the loop top, and the
-//         hops k, k+1 each refill thread kept) over P(k-9), P(k-8)
+//   ring  RS = 2T - 1 + 2F hops: iteration t reads hops k-7 .. k+1 (frames k, k+1) while its
+//         FFT waves write hops k+2, k+3 (prefetched at the loop top) over hops k-9, k-8
 //   Y     [2][F][NW][576] float2, iteration t writes buffer t & 1, its select reads (t - 1) & 1
 // Registers: the FFT path holds the PFB taps and the 512-point sub-FFT, the select path two
 // channels' low-pass state; branches are wave-uniform, so the two live sets do not add up.
 // Measured and dropped: LDS progress words instead of the barrier on three Y
 // buffers (+5.6 %), roles alternating by age on each SIMD (+2.6 %), issue priority for either
-// group or for the younger wave of a pair (zero-sum), non-temporal raw / phase stores (+1.3 %).
+// group or for the younger wave of a pair (zero-sum), non-temporal raw / phase stores (+1.3 %);
+// round 4: a pair ring ((x[s], x[s+2]) pair words built once per sample at refill, -8.5 % VALU
+// instructions: neutral) and buffer-descriptor select I/O (+2.6 %), commit 21e0b7c.
 
-template <int N>
+template <int N, int FW_>
 struct G3 {
     static constexpr int NW = N / 512;
-    static constexpr int FW = 8;                       // transform waves
-    static constexpr int F = FW / NW;                  // frames per iteration
-    static constexpr int BT = 1024;
-    static constexpr int SPT = BT - FW * 64;           // select threads
+    static constexpr int FW = FW_;                     // transform waves (8: one sub-FFT each; 4: sub-FFT w of both frames)
+    static constexpr int F = 2;                        // frames per iteration
+    static constexpr int SPT = 512;                    // select threads (8 waves)
+    static constexpr int BT = FW * 64 + SPT;
     static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
     static constexpr int CPT = C / SPT;                // channels per select thread
-    static constexpr int RS = 2 * T - 1 + F;           // ring slots (pair-hops of M x 8 B)
+    static constexpr int RS = 2 * T - 1 + 2 * F;       // ring slots (hops)
     static constexpr int REG = 576;
     static constexpr int FB = NW * REG;
-    static constexpr size_t off_fbuf = (size_t)RS * M * 8;
+    static constexpr size_t off_fbuf = (size_t)RS * M * 4;
     static constexpr int NB = 2;                       // Y buffers
     static constexpr size_t off_tw1 = off_fbuf + (size_t)NB * F * FB * 8;
     static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;
     static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
-    static_assert(N == 2048 && F == 2 && CPT == 2 && F * M == FW * 64 * 4 && T == 4, "k_front3 geometry");
+    static_assert(N == 2048 && CPT == 2 && (FW == 8 || FW == 4), "k_front3 geometry");
     static_assert(lds_bytes <= 160 * 1024, "LDS");
 };
 
@@ -80,12 +71,12 @@ struct G3 {
 #define STAMP3(slot_) ((void)0)
 #endif
 
-template <int N>
-__global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
-    using G = G3<N>;
-    constexpr int NW = G::NW, M = G::M, C = G::C, RS = G::RS, F = G::F, CPT = G::CPT;
+template <int N, int FW>
+__global__ __launch_bounds__((G3<N, FW>::BT), (G3<N, FW>::BT / 256)) void k_front3(FrontArgs a) {
+    using G = G3<N, FW>;
+    constexpr int NW = G::NW, M = G::M, C = G::C, T = G::T, RS = G::RS, F = G::F, CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint2* ring = reinterpret_cast<uint2*>(smem);
+    uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
     float2* fbuf = reinterpret_cast<float2*>(smem + G::off_fbuf);
     float2* tw1 = reinterpret_cast<float2*>(smem + G::off_tw1);
     float2* tw2 = reinterpret_cast<float2*>(smem + G::off_tw2);
@@ -118,22 +109,20 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
     const int nit = (nrun + kLpfHist + F - 1) / F;    // iterations of F frames from k_start
 
     if (xform) {
-        // ---------------- transform waves: PFB + 512-point sub-FFT of (frame slot, w) ----------
-        const int slot = rw / NW, w = rw % NW;
-        // refill: waves 0-3 (qh = 0) own the even hop of each pair of new hops, waves 4-7 the odd
-        // one; thread g' of its hop loads samples 4 i .. 4 i + 3, i = pair_owner_index(g')
-        const int qh = rw >> 2, gp = (rw & 3) * 64 + L;
-        const int xl = qh * (M / 4) + pair_owner_index(gp);   // front_load4 index: sample 4 xl of the 2 hops
-        uint4 prev = make_uint4(0, 0, 0, 0);                   // hop h - 2 at the same offsets
-        {   // prologue: hops k_start - 7 .. k_start + 1 -> P(k_start - 7) .. P(k_start - 1); hop
-            // k_start - 8 (qh = 0, m = 0) is neither needed nor inside the history
-#pragma unroll
-            for (int m = 0; m <= 4; ++m) {
-                if (qh == 0 && m == 0) continue;
-                const uint4 cur = front_load4<M>(a, k_start - 8 + 2 * m, xl);
-                const int64_t s_ = k_start - 10 + 2 * m + qh;   // pair-hop of (h - 2, h)
-                if (m > 0 && s_ >= k_start - 7) pair_put(ring + (int)(((s_ % RS) + RS) % RS) * M, gp, prev, cur);
-                prev = cur;
+      if constexpr (FW == 4) {
+        // ---- transform waves (FW = 4, one per SIMD): PFB + 512-point sub-FFT w of BOTH frames of
+        // the iteration, the two chains interleaved (independent instructions for the wave's own
+        // dependency and LDS latencies; no older / younger transform wave pair sharing a SIMD).
+        // Frames k and k + 1 read hops k - 7 .. k + 1 at the same plane offsets: the 9 hops' words are
+        // read once (18 ds_read_b64 for 2 sub-FFTs instead of 32), and the I/Q pairs of the hops the
+        // two frames share (frame k's hi = 1 points, frame k + 1's hi = 0 points) are built once.
+        const int w = rw;
+        const int xt = rw * 64 + L;                            // 0 .. 255: samples 4 xt .. 4 xt + 3 of a hop
+        {   // prologue: hops k_start - 7 .. k_start + 1
+            for (int h = 0; h < 2 * T - 1 + F; ++h) {
+                const int64_t hop = k_start - 2 * T + 1 + h;
+                const uint4 v = front_load4<M>(a, hop, xt);
+                ring3_put(ring + (int)(((hop % RS) + RS) % RS) * M, 4 * xt, v);
             }
         }
         uint2 tq[8];
@@ -142,7 +131,149 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
         const int la = L & 7, kl = L >> 3;
         const float2* t1 = tw1 + L;
         const float2* t2 = tw2 + la;
-        int rb = (int)((((k_start - 7) % RS) + RS) % RS);   // slot of P(k - 7)
+        int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);   // slot of hop k - 2T + 1
+        __syncthreads();
+        float2 w1[7], w2[7];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            w1[k - 1] = t1[64 * (k - 1)];
+            w2[k - 1] = t2[8 * (k - 1)];
+            asm volatile("" : "+v"(w1[k - 1].x), "+v"(w1[k - 1].y), "+v"(w2[k - 1].x), "+v"(w2[k - 1].y));
+        }
+        for (int t = 0; t <= nit; ++t) {
+            STAMP3(0);
+            if (t < nit) {
+                const int kr = -kLpfHist + F * t;
+                // the two hops iteration t + 1 adds: loaded now, written after the sub-FFTs
+                const uint4 pre0 = front_load4<M>(a, k_b + kr + F, xt);
+                const uint4 pre1 = front_load4<M>(a, k_b + kr + F + 1, xt);
+                float2* reg0 = fbuf + ((t % G::NB) * F + 0) * G::FB + w * G::REG;
+                float2* reg1 = reg0 + G::FB;
+                // X[h][j]: hop k - 7 + h, plane w, index 64 j + L
+                uint32_t X[2 * T + 1][4];
+#pragma unroll
+                for (int h = 0; h < 2 * T + 1; ++h) {
+                    int sl = rb + h;
+                    sl -= sl >= RS ? RS : 0;
+                    const uint32_t* pl = ring + sl * M + w * (M / NW) + 2 * L;
+                    const uint2 p01 = *reinterpret_cast<const uint2*>(pl);
+                    const uint2 p23 = *reinterpret_cast<const uint2*>(pl + 128);
+                    X[h][0] = p01.x;
+                    X[h][1] = p01.y;
+                    X[h][2] = p23.x;
+                    X[h][3] = p23.y;
+                }
+                // point r = 4 hi + j of frame f takes tap tau from hop 2 tau + hi + f
+                float2 v0[8], v1[8];
+#pragma unroll
+                for (int par = 0; par < 3; ++par)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t i01 = __builtin_amdgcn_perm(X[par + 2][j], X[par][j], kPermI);
+                        const uint32_t q01 = __builtin_amdgcn_perm(X[par + 2][j], X[par][j], kPermQ);
+                        const uint32_t i23 = __builtin_amdgcn_perm(X[par + 6][j], X[par + 4][j], kPermI);
+                        const uint32_t q23 = __builtin_amdgcn_perm(X[par + 6][j], X[par + 4][j], kPermQ);
+#pragma unroll
+                        for (int f = 0; f < 2; ++f) {
+                            const int hi = par - f;
+                            if (hi < 0 || hi > 1) continue;
+                            const int r = 4 * hi + j;
+                            int32_t ai = dot2_first(tq[r].x, i01);
+                            ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
+                            int32_t aq = dot2_first(tq[r].x, q01);
+                            aq = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(q23), aq, false);
+                            (f ? v1 : v0)[r] = make_float2((float)ai, (float)aq);
+                        }
+                    }
+                dft<8>(v0);
+                dft<8>(v1);
+#pragma unroll
+                for (int k = 1; k < 8; ++k) {
+                    v0[k] = cmul_pk(v0[k], w1[k - 1]);
+                    v1[k] = cmul_pk(v1[k], w1[k - 1]);
+                }
+                // T1 of both frames through their regions
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    reg0[72 * r + L] = v0[r];
+                    reg1[72 * r + L] = v1[r];
+                }
+                __builtin_amdgcn_wave_barrier();
+                {
+                    const float2* rd0 = reg0 + 72 * (L >> 3) + (L & 7);
+                    const float2* rd1 = reg1 + 72 * (L >> 3) + (L & 7);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        v0[r] = rd0[8 * r];
+                        v1[r] = rd1[8 * r];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                dft<8>(v0);
+                dft<8>(v1);
+#pragma unroll
+                for (int k = 1; k < 8; ++k) {
+                    v0[k] = cmul_pk(v0[k], w2[k - 1]);
+                    v1[k] = cmul_pk(v1[k], w2[k - 1]);
+                }
+                // T2 of both frames
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    reg0[72 * kl + la + 9 * r] = v0[r];
+                    reg1[72 * kl + la + 9 * r] = v1[r];
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    v0[r] = reg0[72 * kl + 9 * la + r];
+                    v1[r] = reg1[72 * kl + 9 * la + r];
+                }
+                dft<8>(v0);
+                dft<8>(v1);
+                __builtin_amdgcn_wave_barrier();
+                {
+                    const int yo = (kl + 8 * la) ^ (la << 1);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        reg0[yo + 64 * r] = v0[r];
+                        reg1[yo + 64 * r] = v1[r];
+                    }
+                }
+                // ring refill: hops k+2, k+3 over hops k-9, k-8 (no reader this iteration)
+                int ws = rb + 2 * T - 1 + F;
+                ws -= ws >= RS ? RS : 0;
+                int ws1 = ws + 1;
+                ws1 -= ws1 >= RS ? RS : 0;
+                ring3_put(ring + ws * M, 4 * xt, pre0);
+                ring3_put(ring + ws1 * M, 4 * xt, pre1);
+                rb += F;
+                rb -= rb >= RS ? RS : 0;
+            }
+            STAMP3(1);
+            __syncthreads();
+            STAMP3(2);
+        }
+      } else {
+        // ---------------- transform waves: PFB + 512-point sub-FFT of (frame slot, w) ----------
+        const int slot = rw / NW, w = rw % NW;
+        const int xt = rw * 64 + L;                            // thread index among the transform waves
+        const int qh = (xt * 4) / M, qoff = (xt * 4) % M;      // this thread's ring write
+        {   // prologue: hops k_start-2T+1 .. k_start+F-1
+            const int64_t h0 = k_start - 2 * T + 1;
+            for (int g = 0; g < 2 * T - 1 + F; g += 2) {
+                const int64_t hop = h0 + g + qh;
+                if (hop > h0 + 2 * T - 2 + F) continue;
+                const uint4 v = front_load4<M>(a, h0 + g, xt);
+                ring3_put(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
+            }
+        }
+        uint2 tq[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
+        const int la = L & 7, kl = L >> 3;
+        const float2* t1 = tw1 + L;
+        const float2* t2 = tw2 + la;
+        int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);   // slot of hop k - 2T + 1
         __syncthreads();
         // the lane's 14 twiddles are the same every iteration: held in VGPRs (the transform path
         // has registers to spare), 14 fewer LDS reads per sub-FFT on an LDS that is ~60 % busy
@@ -158,30 +289,35 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
             if (t < nit) {
                 const int kr = -kLpfHist + F * t;
                 // the hops iteration t + 1 adds: loaded now, written after this wave's PFB
-                const uint4 pre = front_load4<M>(a, k_b + kr + F, xl);
+                const uint4 pre = front_load4<M>(a, k_b + kr + F, xt);
                 float2* reg = fbuf + ((t % G::NB) * F + slot) * G::FB + w * G::REG;
                 int sb = rb + slot;
                 sb -= sb >= RS ? RS : 0;
-                // pair words of points 4 hi + 2 jp + {0, 1} from P(s) (taps 0, 1) and P(s + 4)
-                // (taps 2, 3), s = k + slot - 7 + hi: 8 ds_read_b128
-                uint4 pw[2][2][2];
+                float2 v[8];
+                uint32_t xr[8][T];
 #pragma unroll
                 for (int hi = 0; hi < 2; ++hi)
 #pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        int sl = sb + hi + 4 * e;
+                    for (int tau = 0; tau < T; ++tau) {
+                        int sl = sb + 2 * tau + hi;
                         sl -= sl >= RS ? RS : 0;
-                        const uint4* pl = reinterpret_cast<const uint4*>(ring + sl * M + w * (M / NW)) + L;
-                        pw[hi][0][e] = pl[0];
-                        pw[hi][1][e] = pl[64];
+                        const uint32_t* pl = ring + sl * M + w * (M / NW) + 2 * L;
+                        const uint2 p01 = *reinterpret_cast<const uint2*>(pl);
+                        const uint2 p23 = *reinterpret_cast<const uint2*>(pl + 128);
+                        xr[4 * hi + 0][tau] = p01.x;
+                        xr[4 * hi + 1][tau] = p01.y;
+                        xr[4 * hi + 2][tau] = p23.x;
+                        xr[4 * hi + 3][tau] = p23.y;
                     }
-                float2 v[8];
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
-                    const uint4& p0 = pw[r >> 2][(r >> 1) & 1][0];
-                    const uint4& p1 = pw[r >> 2][(r >> 1) & 1][1];
-                    const uint32_t i01 = (r & 1) ? p0.z : p0.x, q01 = (r & 1) ? p0.w : p0.y;
-                    const uint32_t i23 = (r & 1) ? p1.z : p1.x, q23 = (r & 1) ? p1.w : p1.y;
+                    uint32_t x4[T];
+#pragma unroll
+                    for (int tau = 0; tau < T; ++tau) x4[tau] = xr[r][tau];
+                    const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermI);
+                    const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermQ);
+                    const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermI);
+                    const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermQ);
                     int32_t ai = dot2_first(tq[r].x, i01);
                     ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
                     int32_t aq = dot2_first(tq[r].x, q01);
@@ -207,12 +343,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
 #pragma unroll
                 for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
-                // ring refill: P(k + qh) = (hop k + qh, hop k + 2 + qh) into the slot of P(k - 9 + qh)
-                // (no reader this iteration)
-                int ws = rb + 7 + qh;
+                // ring refill: hops k+F .. k+2F-1 over hops k-2T-1 .. (no reader this iteration)
+                int ws = rb + 2 * T - 1 + F + qh;
                 ws -= ws >= RS ? RS : 0;
-                pair_put(ring + ws * M, gp, prev, pre);
-                prev = pre;
+                ws -= ws >= RS ? RS : 0;
+                ring3_put(ring + ws * M, qoff, pre);
                 rb += F;
                 rb -= rb >= RS ? RS : 0;
             }
@@ -220,6 +355,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
             __syncthreads();
             STAMP3(2);
         }
+      }
     } else {
         // ---------------- select waves: channels st + SPT q, one iteration behind ---------------
         const int st = rw * 64 + L;
@@ -259,11 +395,6 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
         for (int q = 0; q < CPT; ++q) ys[q] = make_float2(0.f, 0.f);
         int16_t* const raw_run = a.raw + (k_b >> 1) * C;
         float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
-        // the run's outputs (<= 2048 rows x C) and the LO table (P x C float2 = 512 KiB) through
-        // buffer descriptors: row offsets in SGPRs, the lanes' channel offsets loop-invariant
-        const __amdgpu_buffer_rsrc_t raw_rs = buf_rsrc(raw_run);
-        const __amdgpu_buffer_rsrc_t ph_rs = buf_rsrc(phase_run ? phase_run : a.phase);
-        const __amdgpu_buffer_rsrc_t lo_rs = buf_rsrc(a.lo);
         int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
         __syncthreads();
         for (int t = 0; t <= nit; ++t) {
@@ -273,9 +404,9 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 float2 lov[F][CPT];
 #pragma unroll
                 for (int f = 0; f < F; ++f) {
-                    const uint32_t row = (uint32_t)(((lrow + f) & (a.P - 1)) * C) * 8u;
+                    const float2* row = a.lo + ((lrow + f) & (a.P - 1)) * C;
 #pragma unroll
-                    for (int q = 0; q < CPT; ++q) lov[f][q] = buf_ld_f2(lo_rs, 8u * (uint32_t)cq[q], row);
+                    for (int q = 0; q < CPT; ++q) lov[f][q] = row[cq[q]];
                 }
                 lrow += F;
 #pragma unroll
@@ -318,9 +449,9 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                                 // plain stores: with the slot order a wave's store covers its 64
                                 // channels within 2 (raw) or 4 (phase) lines, merged in L2
 #ifndef MKID_XP_STAMPS   // the timing build keeps its stamps in the phase buffer
-                                if (phase_run) buf_st_f32(ph_rs, 4u * (uint32_t)c, 4u * (uint32_t)(jr * C), ph);
+                                if (phase_run) (phase_run + jr * C)[c] = ph;
 #endif
-                                buf_st_i16(raw_rs, 2u * (uint32_t)c, 2u * (uint32_t)(jr * C), (int16_t)qv);
+                                (raw_run + jr * C)[c] = (int16_t)qv;
                                 if (c == a.iq_ch && a.iqtap) {
                                     a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y[q].x);
                                     a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y[q].y);
@@ -340,11 +471,11 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
     }
 }
 
-template <int N>
+template <int N, int FW>
 static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
-    using G = G3<N>;
+    using G = G3<N, FW>;
     static std::atomic<uint64_t> attr_mask{0};
-    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front3<N>, (int)G::lds_bytes);
+    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front3<N, FW>, (int)G::lds_bytes);
     if (e != hipSuccess) return e;
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
@@ -354,10 +485,13 @@ static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
     fpb = (fpb + G::F - 1) / G::F * G::F;
     a.frames_per_block = fpb;
     const int64_t blocks = (a.K + fpb - 1) / fpb;
-    hipLaunchKernelGGL(k_front3<N>, dim3((unsigned)blocks), dim3(G::BT), G::lds_bytes, s, a);
+    hipLaunchKernelGGL((k_front3<N, FW>), dim3((unsigned)blocks), dim3(G::BT), G::lds_bytes, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_front3(const FrontArgs& a, hipStream_t s) { return launch_front3_n<2048>(a, s); }
+#ifndef MKID_F3_FW
+#define MKID_F3_FW 8
+#endif
+hipError_t launch_front3(const FrontArgs& a, hipStream_t s) { return launch_front3_n<2048, MKID_F3_FW>(a, s); }
 
 }  // namespace mkid

@@ -279,21 +279,6 @@ def test_front2_index_maps_and_lds_layouts(N):
         assert m.horner_combine_f32() < 1e-6
 
 
-def test_front3_pair_ring():
-    """k_front3.hip's pair ring (round 4): the refill's (x[s], x[s + 2]) pair words, built once per
-    sample from the kept previous hop, give every PFB point of every frame bit-exactly (integer
-    emulation against the K1 definition), no slot is overwritten while read, and the refill's
-    ds_write_b64 / the PFB's ds_read_b128 are bank-conflict free on gfx950."""
-    import importlib.util
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    spec = importlib.util.spec_from_file_location('front3_pairs', os.path.join(root, 'tools', 'front3_pairs.py'))
-    m = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(m)
-    assert m.pair_ring_emulation(n_iter=8) == (0, 0)
-    ok = m.layout_ok()
-    assert all(ok.values()), ok
-
-
 def test_resdiff_matches_reference_restatement():
     """The shim's vectorised resonator model equals iqsweep.RESDIFF (lib/iqsweep.py:824-858)."""
     from mkids_sdr_amd.roach import resdiff

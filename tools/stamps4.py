@@ -60,26 +60,28 @@ def main():
         phase.zero_()
         ch.process_device(x, S, phase, ev, ev.numel(), cnt)
         torch.cuda.synchronize()
-    if len(sys.argv) > 3 and sys.argv[3] == 'v3':   # k_front3: waves 0-7 transform, 8-15 select
-        st = phase[:4 * 16 * 8 * 16 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 16)
+    if len(sys.argv) > 3 and sys.argv[3] in ('v3', 'v3f4'):
+        # k_front3: waves 0-7 transform, 8-15 select ('v3f4': 0-3 transform, 4-11 select)
+        nx, nw = (8, 16) if sys.argv[3] == 'v3' else (4, 12)
+        st = phase[:4 * 16 * 8 * 16 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 16)[:, :nw]
         for name, a_, b_ in SEG3:
-            w = slice(0, 8) if a_ < 3 else slice(8, 16)
+            w = slice(0, nx) if a_ < 3 else slice(nx, nw)
             top = 0 if a_ < 3 else 3
             x = st[:, w]
             d = x[:, :, 1:, top] - x[:, :, :-1, a_] if str(b_).startswith('next') else x[:, :, :, b_] - x[:, :, :, a_]
             print('%-52s %8.0f cycles  (min %6d max %6d)' % (name, float(np.mean(d)), int(d.min()), int(d.max())))
-        if st[:, :8, :, 7].any():   # decoupled build: the progress-word waits inside the work segments
+        if nx == 8 and st[:, :8, :, 7].any():   # decoupled build: the progress-word waits inside the work segments
             for name, w, a_, b_ in (('transform waves: progress-word wait (in segment 1)', slice(0, 8), 6, 7),
                                     ('select waves: progress-word wait (in segment 4)', slice(8, 16), 8, 9)):
                 d = st[:, w, :, b_] - st[:, w, :, a_]
                 print('%-52s %8.0f cycles  (min %6d max %6d)' % (name, float(np.mean(d)), int(d.min()), int(d.max())))
         work = st[:, :, :, 1] - st[:, :, :, 0] - (st[:, :, :, 7] - st[:, :, :, 6])
         swork = st[:, :, :, 4] - st[:, :, :, 3] - (st[:, :, :, 9] - st[:, :, :, 8])
-        print('per-wave mean work cycles (waits excluded), transform waves 0-7:',
-              ' '.join('%5.0f' % v for v in work[:, :8].mean(axis=(0, 2))))
-        print('per-wave mean work cycles (waits excluded), select waves 8-15:   ',
-              ' '.join('%5.0f' % v for v in swork[:, 8:].mean(axis=(0, 2))))
-        it = st[:, :8, 1:, 0] - st[:, :8, :-1, 0]
+        print('per-wave mean work cycles (waits excluded), transform waves:',
+              ' '.join('%5.0f' % v for v in work[:, :nx].mean(axis=(0, 2))))
+        print('per-wave mean work cycles (waits excluded), select waves:   ',
+              ' '.join('%5.0f' % v for v in swork[:, nx:].mean(axis=(0, 2))))
+        it = st[:, :nx, 1:, 0] - st[:, :nx, :-1, 0]
         print('%-52s %8.0f cycles' % ('iteration (2 frames)', float(np.mean(it))))
         ch.close()
         return

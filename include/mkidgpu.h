@@ -142,7 +142,9 @@ int mkid_reset_stream(mkid_ctx* ctx);
  * receives [nsamples/N][C] float32 rad; events_out receives up to cap packets, channel-major and
  * time-ascending within a channel over the whole call (a call longer than cfg.max_chunk runs as
  * max_chunk pieces whose lists are merged on the host); *nevents = packets produced (> cap =>
- * MKID_E_OVERFLOW; the packets kept are then the first cap in time of each piece). */
+ * MKID_E_OVERFLOW; the packets kept are then the first cap entries of the pieces' channel-major
+ * lists concatenated in piece order: earlier pieces whole, the low channels of the piece that
+ * overflows, nothing of later pieces; merged channel-major as above). */
 int mkid_process(mkid_ctx* ctx, const int16_t* iq, int64_t nsamples, float* phase_out,
                  uint64_t* events_out, int64_t cap, int64_t* nevents);
 

@@ -270,3 +270,18 @@ def reference_bram_words(ref_packets):
 
 
 END_OF_SECOND = np.uint64(0xFFFFFFFFFFFFFFFF)   # PacketMaster.c:331-337 (adr 255, all ones)
+
+
+def py2_str(x):
+    """str(x) of a float as Python 2 printed it (and the reference's text files hold, e.g.
+    ch_noifreqs_0.txt, ch_snap_0.txt: ROACH_Pulses.py:476-536 write str(q) per line): repr at 12
+    significant digits, '.0' kept on integral values."""
+    v = float(x)
+    if v != v:
+        return 'nan'
+    if v in (float('inf'), float('-inf')):
+        return 'inf' if v > 0 else '-inf'
+    t = '%.12g' % v
+    if '.' not in t and 'e' not in t:
+        t += '.0'
+    return t

@@ -34,12 +34,13 @@ __device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
 // buffers (+5.6 %), roles alternating by age on each SIMD (+2.6 %), issue priority for either
 // group or for the younger wave of a pair (zero-sum), non-temporal raw / phase stores (+1.3 %);
 // round 4: a pair ring ((x[s], x[s+2]) pair words built once per sample at refill, -8.5 % VALU
-// instructions: neutral) and buffer-descriptor select I/O (+2.6 %), commit 21e0b7c.
+// instructions: neutral) and buffer-descriptor select I/O (+2.6 %), commit 21e0b7c; 4 transform
+// waves each computing sub-FFT w of both frames, interleaved (+17 %), commit eb8fb42.
 
-template <int N, int FW_>
+template <int N>
 struct G3 {
     static constexpr int NW = N / 512;
-    static constexpr int FW = FW_;                     // transform waves (8: one sub-FFT each; 4: sub-FFT w of both frames)
+    static constexpr int FW = 8;                       // transform waves (one sub-FFT each)
     static constexpr int F = 2;                        // frames per iteration
     static constexpr int SPT = 512;                    // select threads (8 waves)
     static constexpr int BT = FW * 64 + SPT;
@@ -53,7 +54,7 @@ struct G3 {
     static constexpr size_t off_tw1 = off_fbuf + (size_t)NB * F * FB * 8;
     static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;
     static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
-    static_assert(N == 2048 && CPT == 2 && (FW == 8 || FW == 4), "k_front3 geometry");
+    static_assert(N == 2048 && CPT == 2 && F * M == FW * 64 * 4, "k_front3 geometry");
     static_assert(lds_bytes <= 160 * 1024, "LDS");
 };
 
@@ -71,9 +72,9 @@ struct G3 {
 #define STAMP3(slot_) ((void)0)
 #endif
 
-template <int N, int FW>
-__global__ __launch_bounds__((G3<N, FW>::BT), (G3<N, FW>::BT / 256)) void k_front3(FrontArgs a) {
-    using G = G3<N, FW>;
+template <int N>
+__global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
+    using G = G3<N>;
     constexpr int NW = G::NW, M = G::M, C = G::C, T = G::T, RS = G::RS, F = G::F, CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* ring = reinterpret_cast<uint32_t*>(smem);
@@ -109,151 +110,6 @@ __global__ __launch_bounds__((G3<N, FW>::BT), (G3<N, FW>::BT / 256)) void k_fron
     const int nit = (nrun + kLpfHist + F - 1) / F;    // iterations of F frames from k_start
 
     if (xform) {
-      if constexpr (FW == 4) {
-        // ---- transform waves (FW = 4, one per SIMD): PFB + 512-point sub-FFT w of BOTH frames of
-        // the iteration, the two chains interleaved (independent instructions for the wave's own
-        // dependency and LDS latencies; no older / younger transform wave pair sharing a SIMD).
-        // Frames k and k + 1 read hops k - 7 .. k + 1 at the same plane offsets: the 9 hops' words are
-        // read once (18 ds_read_b64 for 2 sub-FFTs instead of 32), and the I/Q pairs of the hops the
-        // two frames share (frame k's hi = 1 points, frame k + 1's hi = 0 points) are built once.
-        const int w = rw;
-        const int xt = rw * 64 + L;                            // 0 .. 255: samples 4 xt .. 4 xt + 3 of a hop
-        {   // prologue: hops k_start - 7 .. k_start + 1
-            for (int h = 0; h < 2 * T - 1 + F; ++h) {
-                const int64_t hop = k_start - 2 * T + 1 + h;
-                const uint4 v = front_load4<M>(a, hop, xt);
-                ring3_put(ring + (int)(((hop % RS) + RS) % RS) * M, 4 * xt, v);
-            }
-        }
-        uint2 tq[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
-        const int la = L & 7, kl = L >> 3;
-        const float2* t1 = tw1 + L;
-        const float2* t2 = tw2 + la;
-        int rb = (int)((((k_start + 1 - 2 * T) % RS) + RS) % RS);   // slot of hop k - 2T + 1
-        __syncthreads();
-        float2 w1[7], w2[7];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) {
-            w1[k - 1] = t1[64 * (k - 1)];
-            w2[k - 1] = t2[8 * (k - 1)];
-            asm volatile("" : "+v"(w1[k - 1].x), "+v"(w1[k - 1].y), "+v"(w2[k - 1].x), "+v"(w2[k - 1].y));
-        }
-        for (int t = 0; t <= nit; ++t) {
-            STAMP3(0);
-            if (t < nit) {
-                const int kr = -kLpfHist + F * t;
-                // the two hops iteration t + 1 adds: loaded now, written after the sub-FFTs
-                const uint4 pre0 = front_load4<M>(a, k_b + kr + F, xt);
-                const uint4 pre1 = front_load4<M>(a, k_b + kr + F + 1, xt);
-                float2* reg0 = fbuf + ((t % G::NB) * F + 0) * G::FB + w * G::REG;
-                float2* reg1 = reg0 + G::FB;
-                // X[h][j]: hop k - 7 + h, plane w, index 64 j + L
-                uint32_t X[2 * T + 1][4];
-#pragma unroll
-                for (int h = 0; h < 2 * T + 1; ++h) {
-                    int sl = rb + h;
-                    sl -= sl >= RS ? RS : 0;
-                    const uint32_t* pl = ring + sl * M + w * (M / NW) + 2 * L;
-                    const uint2 p01 = *reinterpret_cast<const uint2*>(pl);
-                    const uint2 p23 = *reinterpret_cast<const uint2*>(pl + 128);
-                    X[h][0] = p01.x;
-                    X[h][1] = p01.y;
-                    X[h][2] = p23.x;
-                    X[h][3] = p23.y;
-                }
-                // point r = 4 hi + j of frame f takes tap tau from hop 2 tau + hi + f
-                float2 v0[8], v1[8];
-#pragma unroll
-                for (int par = 0; par < 3; ++par)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint32_t i01 = __builtin_amdgcn_perm(X[par + 2][j], X[par][j], kPermI);
-                        const uint32_t q01 = __builtin_amdgcn_perm(X[par + 2][j], X[par][j], kPermQ);
-                        const uint32_t i23 = __builtin_amdgcn_perm(X[par + 6][j], X[par + 4][j], kPermI);
-                        const uint32_t q23 = __builtin_amdgcn_perm(X[par + 6][j], X[par + 4][j], kPermQ);
-#pragma unroll
-                        for (int f = 0; f < 2; ++f) {
-                            const int hi = par - f;
-                            if (hi < 0 || hi > 1) continue;
-                            const int r = 4 * hi + j;
-                            int32_t ai = dot2_first(tq[r].x, i01);
-                            ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
-                            int32_t aq = dot2_first(tq[r].x, q01);
-                            aq = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(q23), aq, false);
-                            (f ? v1 : v0)[r] = make_float2((float)ai, (float)aq);
-                        }
-                    }
-                dft<8>(v0);
-                dft<8>(v1);
-#pragma unroll
-                for (int k = 1; k < 8; ++k) {
-                    v0[k] = cmul_pk(v0[k], w1[k - 1]);
-                    v1[k] = cmul_pk(v1[k], w1[k - 1]);
-                }
-                // T1 of both frames through their regions
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    reg0[72 * r + L] = v0[r];
-                    reg1[72 * r + L] = v1[r];
-                }
-                __builtin_amdgcn_wave_barrier();
-                {
-                    const float2* rd0 = reg0 + 72 * (L >> 3) + (L & 7);
-                    const float2* rd1 = reg1 + 72 * (L >> 3) + (L & 7);
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        v0[r] = rd0[8 * r];
-                        v1[r] = rd1[8 * r];
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                dft<8>(v0);
-                dft<8>(v1);
-#pragma unroll
-                for (int k = 1; k < 8; ++k) {
-                    v0[k] = cmul_pk(v0[k], w2[k - 1]);
-                    v1[k] = cmul_pk(v1[k], w2[k - 1]);
-                }
-                // T2 of both frames
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    reg0[72 * kl + la + 9 * r] = v0[r];
-                    reg1[72 * kl + la + 9 * r] = v1[r];
-                }
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    v0[r] = reg0[72 * kl + 9 * la + r];
-                    v1[r] = reg1[72 * kl + 9 * la + r];
-                }
-                dft<8>(v0);
-                dft<8>(v1);
-                __builtin_amdgcn_wave_barrier();
-                {
-                    const int yo = (kl + 8 * la) ^ (la << 1);
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        reg0[yo + 64 * r] = v0[r];
-                        reg1[yo + 64 * r] = v1[r];
-                    }
-                }
-                // ring refill: hops k+2, k+3 over hops k-9, k-8 (no reader this iteration)
-                int ws = rb + 2 * T - 1 + F;
-                ws -= ws >= RS ? RS : 0;
-                int ws1 = ws + 1;
-                ws1 -= ws1 >= RS ? RS : 0;
-                ring3_put(ring + ws * M, 4 * xt, pre0);
-                ring3_put(ring + ws1 * M, 4 * xt, pre1);
-                rb += F;
-                rb -= rb >= RS ? RS : 0;
-            }
-            STAMP3(1);
-            __syncthreads();
-            STAMP3(2);
-        }
-      } else {
         // ---------------- transform waves: PFB + 512-point sub-FFT of (frame slot, w) ----------
         const int slot = rw / NW, w = rw % NW;
         const int xt = rw * 64 + L;                            // thread index among the transform waves
@@ -355,7 +211,6 @@ __global__ __launch_bounds__((G3<N, FW>::BT), (G3<N, FW>::BT / 256)) void k_fron
             __syncthreads();
             STAMP3(2);
         }
-      }
     } else {
         // ---------------- select waves: channels st + SPT q, one iteration behind ---------------
         const int st = rw * 64 + L;
@@ -471,11 +326,11 @@ __global__ __launch_bounds__((G3<N, FW>::BT), (G3<N, FW>::BT / 256)) void k_fron
     }
 }
 
-template <int N, int FW>
+template <int N>
 static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
-    using G = G3<N, FW>;
+    using G = G3<N>;
     static std::atomic<uint64_t> attr_mask{0};
-    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front3<N, FW>, (int)G::lds_bytes);
+    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front3<N>, (int)G::lds_bytes);
     if (e != hipSuccess) return e;
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
@@ -485,13 +340,10 @@ static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
     fpb = (fpb + G::F - 1) / G::F * G::F;
     a.frames_per_block = fpb;
     const int64_t blocks = (a.K + fpb - 1) / fpb;
-    hipLaunchKernelGGL((k_front3<N, FW>), dim3((unsigned)blocks), dim3(G::BT), G::lds_bytes, s, a);
+    hipLaunchKernelGGL(k_front3<N>, dim3((unsigned)blocks), dim3(G::BT), G::lds_bytes, s, a);
     return hipGetLastError();
 }
 
-#ifndef MKID_F3_FW
-#define MKID_F3_FW 8
-#endif
-hipError_t launch_front3(const FrontArgs& a, hipStream_t s) { return launch_front3_n<2048, MKID_F3_FW>(a, s); }
+hipError_t launch_front3(const FrontArgs& a, hipStream_t s) { return launch_front3_n<2048>(a, s); }
 
 }  // namespace mkid

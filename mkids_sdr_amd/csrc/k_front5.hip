@@ -154,8 +154,8 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             int cb = c0;
             asm volatile("" : "+v"(cb));
             const float2* yf = fbuf + f * G5::FB;
-            // LO values one frame ahead (the global-load latency hides behind a frame of work); the
-            // centres of an output frame are loaded at its start
+            // the LO row of this frame is loaded at the frame's start (loading it a frame ahead was
+            // measured flat, DESIGN.md §5 k_front5); the centres of an output frame likewise
             float2 lov[CPT];
             {
                 const char* lorow = reinterpret_cast<const char*>(a.lo + ((lrow + f) & (a.P - 1)) * C);

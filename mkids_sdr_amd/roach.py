@@ -573,20 +573,31 @@ class RoachPulses:
                    median=float(np.median(phase)), mean=float(np.mean(phase)), std=float(np.std(phase)))
         if save_dir is not None:
             import os
+            from datetime import datetime
             os.makedirs(save_dir, exist_ok=True)
+            # the reference writes str(q) per line (Python 2: 12 significant digits, codecs.py2_str)
             for name, arr in (('ch_out', qdr_phase), ('ch_snap', phase), ('ch_noifreqs', freqs),
                               ('ch_noise', noise)):
                 with open(os.path.join(save_dir, '%s_%d.txt' % (name, ch)), 'w') as f:
-                    f.writelines('%r\n' % float(q) for q in arr)
+                    f.writelines(codecs.py2_str(q) + '\n' for q in arr)
+            # and the qdr phase once more under LongSnapShots/ with numpy.savetxt fmt='%.8f'
+            # (ROACH_Pulses.py:489-498)
+            ls_dir = os.path.join(save_dir, 'LongSnapShots')
+            os.makedirs(ls_dir, exist_ok=True)
+            out['longsnapshot_file'] = os.path.join(
+                ls_dir, 'longsnapshot_' + datetime.utcnow().strftime('%Y-%m-%d_%H%M%S%f')[:-3] + '.txt')
+            np.savetxt(out['longsnapshot_file'], qdr_phase, fmt='%.8f')
         return out
 
     def contsnapshot(self, ch, steps=1, phase_threshold=-20.0, averagelength_power=10, maxloops=None,
-                     cap=4096):
+                     cap=None):
         """ROACH_Pulses.py:557-762: qdr0 snapshot(s) of channel ch in degrees, then the block-mean
         trigger over it (means of 2^averagelength_power-sample blocks, start 500, hit when
         |mean - x| > phase_threshold, skip 1000, stop at bob + 1500 > len: 614-727) — run on the
         device (mkid_replay_trigger) — and the 2000-sample window [bob-500, bob+1500) of every hit.
-        The reference's loop also stops after `maxloops` passes (failsafe, 747-750); None = no cap.
+        The reference's loop also stops after `maxloops` passes (failsafe, 747-750; its first pass
+        always runs, so maxloops <= 1 means one pass); None = no cap. `cap` bounds the device hit list
+        (default: every hit the capture can hold, one per 1000 samples, or the pass bound).
         Returns dict(pulsenumber, phase (the two columns it saves, '%i %.2f'), hits, total_pulses,
         qdr_phase (the snapshot in degrees))."""
         import torch
@@ -596,12 +607,20 @@ class RoachPulses:
         dev = c.torch_device()
         d_raw = torch.from_numpy(qdr_raw.astype(np.int16)).to(dev)
         torch.cuda.synchronize(dev)
+        if cap is None:
+            # a hit skips 1000 samples: at most len/1000 + 2 of them; with maxloops at most that
+            # many passes, each with at most one hit
+            cap = len(qdr_raw) // 1000 + 2
+            if maxloops is not None:
+                cap = min(cap, max(int(maxloops), 1) + 1)
         hits = replay.block_mean_trigger(c, d_raw, len(qdr_raw), 1, 1, averagelength=2 ** int(averagelength_power),
                                          threshold=float(phase_threshold), start=500, need=1500, skip=1000,
                                          wrap_negative=False, cap=cap)[0]
         if maxloops is not None:
-            # pass index of the k-th hit (0-based): every pass advances bob by 1, a hit by 1000
-            hits = [h for k, h in enumerate(hits) if (h - 500) - 999 * k < int(maxloops)]
+            # pass index of the k-th hit (0-based): every pass advances bob by 1, a hit by 1000;
+            # the failsafe breaks after pass failsafe > maxloops - 1, so pass 0 always runs
+            passes = max(int(maxloops), 1)
+            hits = [h for k, h in enumerate(hits) if (h - 500) - 999 * k < passes]
         pulsenumber = [0.0] * 2000                  # pulse 0's numbers: the initial zeros (560-561)
         final = []
         for k, h in enumerate(hits):

@@ -241,15 +241,28 @@ def test_longsnapshot_and_contsnapshot(gpu, tmp_path):
     assert np.array_equal(f2, ls['noiseFFTFreqs'])
     assert np.allclose(ls['noiseFFT'], n2, rtol=1e-12, atol=1e-9)
     assert np.isfinite(ls['noiseFFT'][1:]).all()
-    assert np.allclose(np.loadtxt(str(tmp_path / 'ch_noifreqs_0.txt')), ref_freqs, atol=1e-12)
+    # the saved files are the reference's text: str(q) per line, Python 2 (12 significant digits);
+    # the bins file is byte-identical to the reference's own ch_noifreqs_0.txt
+    assert open(str(tmp_path / 'ch_noifreqs_0.txt')).read() == open(os.path.join(GOLD, 'ch_noifreqs_0.txt')).read()
+    assert np.allclose(np.loadtxt(ls['longsnapshot_file']), ls['qdr_phase'], rtol=0, atol=5e-9)
     # noise only: a threshold of a few degrees fires on the noise tails
     sd = float(np.std(ls['qdr_phase']))
     thr = 3.5 * sd
-    for maxloops in (None, 200000):
+    for maxloops in (None, 200000, 3000):
         cs = rp.contsnapshot(0, steps=1, phase_threshold=thr, averagelength_power=10, maxloops=maxloops)
         qdr = cs['qdr_phase']
-        hits, pn, fin = oreplay.contsnapshot_loop(qdr, thr, 1024, maxloops or (1 << 40))
+        hits, pn, fin = oreplay.contsnapshot_loop(qdr, thr, 1024, (1 << 40) if maxloops is None else maxloops)
         assert cs['hits'] == hits
         assert cs['pulsenumber'] == pn
         assert np.array_equal(np.asarray(cs['phase']), np.asarray(fin))
-        assert len(hits) > 3
+        assert len(hits) > 3 or maxloops == 3000
+    # the reference's default threshold (-20: every pass hits) over 4 snapshots (2^22 samples, ~4190
+    # hits, more than any fixed cap), and a failsafe of 0 / 1 pass (the first pass always runs,
+    # ROACH_Pulses.py:747-750)
+    for steps, maxloops in ((4, None), (1, 0), (1, 1)):
+        cs = rp.contsnapshot(0, steps=steps, phase_threshold=-20.0, averagelength_power=10, maxloops=maxloops)
+        hits, pn, fin = oreplay.contsnapshot_loop(cs['qdr_phase'], -20.0, 1024,
+                                                 (1 << 40) if maxloops is None else maxloops)
+        assert cs['hits'] == hits and cs['pulsenumber'] == pn
+        assert np.array_equal(np.asarray(cs['phase']), np.asarray(fin))
+        assert len(hits) == (1 if maxloops is not None else len(cs['qdr_phase']) // 1000 - 1)

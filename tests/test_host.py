@@ -331,3 +331,15 @@ def test_noise_spectrum_matches_reference_loop():
     assert np.allclose(f, ref, rtol=0, atol=1e-12)
     raw = np.array([-25736, -1, 0, 1, 25736, 12345], np.int64)
     assert np.array_equal(codecs.decode_qdr(raw.astype('>i2').tobytes()), raw)
+
+
+def test_py2_str_reproduces_reference_text_files():
+    """The reference writes its snapshot files with Python 2 str(q) per line (ROACH_Pulses.py:476-536);
+    codecs.py2_str reproduces both of the reference's own saved files byte for byte."""
+    from mkids_sdr_amd.codecs import py2_str
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for name in ('ch_noifreqs_0.txt', 'ch_snap_0.txt'):
+        text = open(os.path.join(root, 'tests', 'golden', name)).read()
+        lines = text.splitlines()
+        assert ''.join(py2_str(float(v)) + '\n' for v in lines) == text
+    assert py2_str(0.0) == '0.0' and py2_str(-3.0) == '-3.0' and py2_str(1e-20) == '1e-20'

@@ -35,7 +35,8 @@ __device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
 // group or for the younger wave of a pair (zero-sum), non-temporal raw / phase stores (+1.3 %);
 // round 4: a pair ring ((x[s], x[s+2]) pair words built once per sample at refill, -8.5 % VALU
 // instructions: neutral) and buffer-descriptor select I/O (+2.6 %), commit 21e0b7c; 4 transform
-// waves each computing sub-FFT w of both frames, interleaved (+17 %), commit eb8fb42.
+// waves each computing sub-FFT w of both frames, interleaved (+17 %), commit eb8fb42; two
+// 768-thread workgroups per CU at one frame per iteration (k_front6, +25 %), commit ac8fe74.
 
 template <int N>
 struct G3 {

@@ -597,7 +597,7 @@ class RoachPulses:
         device (mkid_replay_trigger) — and the 2000-sample window [bob-500, bob+1500) of every hit.
         The reference's loop also stops after `maxloops` passes (failsafe, 747-750; its first pass
         always runs, so maxloops <= 1 means one pass); None = no cap. `cap` bounds the device hit list
-        (default: every hit the capture can hold, one per 1000 samples, or the pass bound).
+        (default: every hit the capture can hold, one per 1000 samples).
         Returns dict(pulsenumber, phase (the two columns it saves, '%i %.2f'), hits, total_pulses,
         qdr_phase (the snapshot in degrees))."""
         import torch
@@ -608,11 +608,9 @@ class RoachPulses:
         d_raw = torch.from_numpy(qdr_raw.astype(np.int16)).to(dev)
         torch.cuda.synchronize(dev)
         if cap is None:
-            # a hit skips 1000 samples: at most len/1000 + 2 of them; with maxloops at most that
-            # many passes, each with at most one hit
+            # the device walks the whole capture (the failsafe is applied to its hit list below),
+            # and a hit skips 1000 samples: at most len/1000 + 2 hits
             cap = len(qdr_raw) // 1000 + 2
-            if maxloops is not None:
-                cap = min(cap, max(int(maxloops), 1) + 1)
         hits = replay.block_mean_trigger(c, d_raw, len(qdr_raw), 1, 1, averagelength=2 ** int(averagelength_power),
                                          threshold=float(phase_threshold), start=500, need=1500, skip=1000,
                                          wrap_negative=False, cap=cap)[0]

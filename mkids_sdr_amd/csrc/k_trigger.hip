@@ -27,7 +27,7 @@ namespace mkid {
 constexpr int kSpecThreads = 256;
 // full trigger steps at the end of a speculative warm-up (groups of 26 samples): the state machine
 // forgets a guessed start within the dead time plus one threshold crossing; earlier warm-up
-// samples advance only the baseline (the SVF warm-up is ~10^5 samples, the EMA one 520)
+// samples advance only the baseline (the SVF warm-up is ~10^5 samples, the EMA one 260)
 constexpr int32_t kFullWarm = 100;
 
 __device__ __attribute__((noinline)) uint64_t make_packet(int32_t c, EvInfo ev, int32_t f, int64_t jg) {

@@ -18,9 +18,12 @@ constexpr int kPfbTaps = 4;
 
 // Speculative trigger segmentation (k_trigger.hip): segments of at least kSegL phase samples,
 // each speculating from kSegW samples of warm-up (a multiple of the 26-sample matched-filter ring).
-// The EMA baseline (alpha 41/512) forgets its start in ~10^2 samples on noisy phase.
+// The EMA baseline (alpha 41/512) forgets its start in ~10^2 samples on noisy phase. The warm-up is
+// pure overhead when the speculation holds and the fix-up re-runs a segment when it does not
+// (exact either way): on the bench stream 520 -> 260 samples is -6 % trigger time with no re-run,
+// 130 re-runs 427 segments per step and gains nothing (profiles/r04_j_kbench_trig_warmup.json).
 constexpr int64_t kSegL = 2048;
-constexpr int64_t kSegW = 520;
+constexpr int64_t kSegW = 260;
 // SVF baseline (Chamberlin 2-pole, Kf 82 / Kq 93623 Fix18_16): two integer trajectories started
 // from different states coincide only after ~10^4 samples (median 1.5e4, 99th percentile 2.9e4, max
 // 3.9e4 over 1024 simulated noisy channels; on the bench stream a 49k-sample warm-up still missed

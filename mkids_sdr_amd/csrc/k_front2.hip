@@ -341,7 +341,7 @@ static hipError_t launch_front2_n(const FrontArgs& a0, hipStream_t s) {
 }
 
 hipError_t launch_front2(int N, const FrontArgs& a, hipStream_t s) {
-    if (N == 2048 && a.variant == 3) return launch_front3(a, s);
+    if ((N == 2048 || N == 512) && a.variant == 3) return launch_front3(N, a, s);
     switch (N) {
         case 512: return launch_front2_n<512>(a, s);
         case 1024: return launch_front2_n<1024>(a, s);

@@ -1,4 +1,5 @@
-// Fused front end k_front3 (N = 2048, config 3/4; the default at N = 2048): k_front2's arithmetic
+// Fused front end k_front3 (the default at N = 2048, config 3/4, and since round 4 at N = 512,
+// config 2: -5.3 % same-box, profiles/r04_k_kbench_f3_512_vs_f2.json): k_front2's arithmetic
 // (k_front2.hip) with wave specialisation.
 #include "front_common.h"
 
@@ -38,12 +39,16 @@ __device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
 // waves each computing sub-FFT w of both frames, interleaved (+17 %), commit eb8fb42; two
 // 768-thread workgroups per CU at one frame per iteration (k_front6, +25 %), commit ac8fe74.
 
+// Geometry per N. N = 2048 (config 3/4): 8 transform waves (4 sub-FFTs x 2 frames) + 8 select
+// waves (2 channels per thread), one workgroup per CU. N = 512 (config 2, round 4): 4 transform waves
+// (the 512-point FFT of each of 4 frames) + 4 select waves (1 channel per thread), two workgroups
+// per CU.
 template <int N>
 struct G3 {
-    static constexpr int NW = N / 512;
-    static constexpr int FW = 8;                       // transform waves (one sub-FFT each)
-    static constexpr int F = 2;                        // frames per iteration
-    static constexpr int SPT = 512;                    // select threads (8 waves)
+    static constexpr int NW = N / 512;                 // sub-FFTs per frame
+    static constexpr int F = N == 2048 ? 2 : 4;        // frames per iteration
+    static constexpr int FW = F * NW;                  // transform waves (one sub-FFT each)
+    static constexpr int SPT = N == 2048 ? 512 : 256;  // select threads
     static constexpr int BT = FW * 64 + SPT;
     static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
     static constexpr int CPT = C / SPT;                // channels per select thread
@@ -55,9 +60,26 @@ struct G3 {
     static constexpr size_t off_tw1 = off_fbuf + (size_t)NB * F * FB * 8;
     static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;
     static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
-    static_assert(N == 2048 && CPT == 2 && F * M == FW * 64 * 4, "k_front3 geometry");
-    static_assert(lds_bytes <= 160 * 1024, "LDS");
+    static constexpr int WG_PER_CU = 16 * 64 / BT;     // 16 waves per CU
+    static_assert((N == 2048 || N == 512) && F * M == FW * 64 * 4 && C == SPT * CPT, "k_front3 geometry");
+    static_assert(lds_bytes * WG_PER_CU <= 160 * 1024, "LDS");
 };
+
+// ring plane layout for any NW (paired planes of Q = M / NW = 256 samples): samples qoff..qoff+3 of
+// a hop (qoff a multiple of 4) go to plane o mod NW at plane index o / NW
+template <int NW>
+__device__ __forceinline__ void ring3_put_nw(uint32_t* hop, int qoff, uint4 v) {
+    if constexpr (NW == 4) {
+        ring3_put(hop, qoff, v);
+    } else {
+        static_assert(NW == 1, "ring layout");
+        const int a = ring3_idx(qoff);
+        hop[a] = v.x;
+        hop[a + 2] = v.y;
+        hop[a + 4] = v.z;
+        hop[a + 6] = v.w;
+    }
+}
 
 #ifdef MKID_XP_STAMPS
 #define STAMP3(slot_)                                                                             \
@@ -74,7 +96,7 @@ struct G3 {
 #endif
 
 template <int N>
-__global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
+__global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 waves per CU
     using G = G3<N>;
     constexpr int NW = G::NW, M = G::M, C = G::C, T = G::T, RS = G::RS, F = G::F, CPT = G::CPT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -121,7 +143,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 const int64_t hop = h0 + g + qh;
                 if (hop > h0 + 2 * T - 2 + F) continue;
                 const uint4 v = front_load4<M>(a, h0 + g, xt);
-                ring3_put(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
+                ring3_put_nw<NW>(ring + (int)(((hop % RS) + RS) % RS) * M, qoff, v);
             }
         }
         uint2 tq[8];
@@ -204,7 +226,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
                 int ws = rb + 2 * T - 1 + F + qh;
                 ws -= ws >= RS ? RS : 0;
                 ws -= ws >= RS ? RS : 0;
-                ring3_put(ring + ws * M, qoff, pre);
+                ring3_put_nw<NW>(ring + ws * M, qoff, pre);
                 rb += F;
                 rb -= rb >= RS ? RS : 0;
             }
@@ -215,7 +237,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {
     } else {
         // ---------------- select waves: channels st + SPT q, one iteration behind ---------------
         const int st = rw * 64 + L;
-        float2 tl[CPT][NW - 1];
+        float2 tl[CPT][NW > 1 ? NW - 1 : 1];
         int yoff[CPT];
         float ic[CPT], qc[CPT];
         // channel of (thread, q): a host-chosen order (mkid_api.hip slot_order) that puts the 32
@@ -336,7 +358,7 @@ static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
     const int64_t ncu = a.ncu > 0 ? a.ncu : 256;
-    int64_t fpb = a.K / ncu;                     // one run per CU, as k_front2
+    int64_t fpb = a.K / (ncu * G::WG_PER_CU);    // one run per resident workgroup, as k_front2
     fpb = fpb < 64 ? 64 : (fpb > 4096 ? 4096 : fpb);
     fpb = (fpb + G::F - 1) / G::F * G::F;
     a.frames_per_block = fpb;
@@ -345,6 +367,12 @@ static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_front3(const FrontArgs& a, hipStream_t s) { return launch_front3_n<2048>(a, s); }
+hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s) {
+    switch (N) {
+        case 2048: return launch_front3_n<2048>(a, s);
+        case 512: return launch_front3_n<512>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
 
 }  // namespace mkid

@@ -78,7 +78,7 @@ struct mkid_ctx {
     int64_t last_raw_row = 0;       // first row of the last sub-chunk's raw phase in d_raw
     bool fused = false;  // K1-K6 in one kernel (k_front / k_front2 / k_front4: no z buffers, no stream B work)
     bool front_v2 = false;  // fused front end is k_front2 (N = 512..2048; MKID_FRONT_V1=1 forces v1)
-    int front_variant = 3;  // N = 2048: 3 = wave-specialised k_front3 (MKID_FRONT_V3=0: k_front2)
+    int front_variant = 3;  // N = 512 / 2048: 3 = wave-specialised k_front3 (MKID_FRONT_V3=0: k_front2)
     int64_t H = 0;       // ADC history samples carried between calls
     // workspace
     float2* d_zb[2] = {nullptr, nullptr};
@@ -289,6 +289,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
         c->front_v2 = c->fused && front2_supported(N) && !(v1 && atoi(v1) != 0);
         const char* v3 = getenv("MKID_FRONT_V3");
         c->front_variant = (v3 && atoi(v3) == 0) ? 2 : 3;
+
         if (N == 4096) {
             const char* v5 = getenv("MKID_FRONT_V5");
             c->front_variant = (v5 && atoi(v5) == 0) ? 4 : 5;   // k_front5 unless MKID_FRONT_V5=0

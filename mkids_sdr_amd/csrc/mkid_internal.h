@@ -97,7 +97,7 @@ struct FrontArgs {
     LpfTaps taps;
     int16_t* iqtap;         // [K/2][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
     int32_t iq_ch;
-    int32_t variant;        // N = 2048: 3 = wave-specialised k_front3, else k_front2; N = 4096: 5 = k_front5, else k_front4
+    int32_t variant;        // N = 512 / 2048: 3 = wave-specialised k_front3, else k_front2; N = 4096: 5 = k_front5, else k_front4
     const int16_t* slot_ch; // [C] k_front3: channel of select slot st + 512 q (nullptr: identity)
 };
 
@@ -186,7 +186,7 @@ bool channelize_supported(int N);
 bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length
 bool front2_supported(int N);        // the one-exchange fused kernel (k_front2.hip) for this N
 hipError_t launch_front2(int N, const FrontArgs& a, hipStream_t s);
-hipError_t launch_front3(const FrontArgs& a, hipStream_t s);  // N = 2048, wave-specialised (k_front3.hip)
+hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s);  // N = 512 / 2048, wave-specialised (k_front3.hip)
 bool front4_supported(int N);        // the 2048-channel fused kernel (k_front4.hip, N = 4096)
 hipError_t launch_front4(const FrontArgs& a, hipStream_t s);
 hipError_t launch_front5(const FrontArgs& a, hipStream_t s);  // N = 4096, wave-specialised (k_front5.hip)

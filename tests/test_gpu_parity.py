@@ -144,8 +144,8 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     (2048, 2 ** 20, None, 6, 'split'),
 ])
 def test_chain_parity(gpu, C, S, splits, seed, front):
-    """Full chain vs the oracle. 'auto' runs the fused front end (k_front3 for N = 2048, k_front2
-    for N = 512/1024, k_front5 for N = 4096, k_front for N = 128); 'split' runs k_channelize +
+    """Full chain vs the oracle. 'auto' runs the fused front end (k_front3 for N = 512 and 2048,
+    k_front2 for N = 1024, k_front5 for N = 4096, k_front for N = 128); 'split' runs k_channelize +
     k_lpf_phase with z staged in HBM."""
     case, thr = cached_case(C, S, seed, max(1.0, S / (2 * C) / 400))
     compare(case, thr, splits or [0, S], front=front)
@@ -158,6 +158,15 @@ def test_chain_parity_front2_at_2048(gpu, monkeypatch):
     C, S = 1024, 2 ** 20
     case, thr = cached_case(C, S, 5, max(1.0, S / (2 * C) / 400))
     compare(case, thr, [0, 2 ** 19, S])
+
+
+def test_chain_parity_front2_at_512(gpu, monkeypatch):
+    """The non-specialised k_front2 at N = 512 (MKID_FRONT_V3=0; the default there is k_front3<512>
+    since round 4) on config 2's streamed parity case."""
+    monkeypatch.setenv('MKID_FRONT_V3', '0')
+    C, S = 256, 2 ** 18
+    case, thr = cached_case(C, S, 3, max(1.0, S / (2 * C) / 400))
+    compare(case, thr, [0, 2 ** 16 + 512, 2 ** 17, S])
 
 
 def test_chain_parity_front4_at_4096(gpu, monkeypatch):

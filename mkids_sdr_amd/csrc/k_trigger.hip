@@ -101,7 +101,8 @@ __device__ __forceinline__ int32_t mf_q(QWin& w, const uint32_t (&tp)[kFirTaps /
 
 // Software pipeline over half groups of 13 samples: the loads of the next half are in flight
 // while the current half is processed (26 load registers, as for a whole-group batch, but no
-// wave waits a full memory latency per group). body(group, u, raw) sees u = 0..25 in order;
+// wave waits a full memory latency per group). A whole group in flight ahead (52 registers, 2 waves
+// per SIMD) is +16 % at config 3 and flat at config 2 (profiles/r04_l_kbench_trig_deep_c*.json). body(group, u, raw) sees u = 0..25 in order;
 // roff advances by ngroups rows of 26. The last prefetch re-reads the current group (in bounds).
 template <class F>
 __device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, uint32_t& roff,
@@ -125,6 +126,7 @@ __device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, u
         roff += (uint32_t)kFirTaps * row;
     }
 }
+
 
 // The per-sample recurrence of k_trig_spec: the code-state forms trig_update_fast (EMA / no
 // baseline) and trig_update_svf (SVF) on the throughput path, trig_update itself (FAST = false)

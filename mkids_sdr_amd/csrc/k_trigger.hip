@@ -89,42 +89,73 @@ __device__ __forceinline__ void load_qwin(QWin& w, const TrigSpecArgs& a, int c,
 
 // r: the aligned dword holding raw_j (lanes 2k and 2k+1 load the same dword and keep their own
 // half): the pack is one v_perm, and the loaded values stay 32-bit through the pipelined loop
-__device__ __forceinline__ int32_t mf_q(QWin& w, const uint32_t (&tp)[kFirTaps / 2], int u, uint32_t r) {
+// lim: -32768 and 32767 in VGPRs (made opaque by the caller), so that the clamp of mf_out is one
+// v_med3_i32 (gfx9 VOP3 takes no literal operand; with literals it is a v_max + v_min pair)
+struct Lim16 {
+    int32_t lo, hi;
+};
+__device__ __forceinline__ int32_t mf_q(QWin& w, const uint32_t (&tp)[kFirTaps / 2], int u, uint32_t r,
+                                        const Lim16& lim) {
     w.q[u] = __builtin_amdgcn_perm(w.last, r, w.sel);
     w.last = r;
-    int32_t acc = 0;
+    // first product into a zero accumulator (v_dot2_i32_i16 ..., 0): the compiler otherwise zeroes
+    // a register for a v_dot2c chain, one extra VALU per sample
+    int32_t acc;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(acc) : "v"(tp[0]), "v"(w.q[u]));
 #pragma unroll
-    for (int m = 0; m < kFirTaps / 2; ++m)
+    for (int m = 1; m < kFirTaps / 2; ++m)
         acc = __builtin_amdgcn_sdot2(as_s2(tp[m]), as_s2(w.q[(u - 2 * m + 2 * kFirTaps) % kFirTaps]), acc, false);
-    return mf_out(acc);
+    int32_t v;   // mf_out: clamp16(acc >> 11)
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(v) : "v"(acc >> 11), "v"(lim.lo), "v"(lim.hi));
+    return v;
+}
+
+// Buffer loads of the raw phase: the row offset rrow is wave-uniform (the instruction's SGPR offset,
+// no VALU address arithmetic per load), lane the lane's constant byte offset. The descriptor
+// spans 4 GiB from the wave's segment base (word 3 as ck_tile's gfx9 buffer resource).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const char* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, (int)0xffffffff, 0x00020000);
 }
 
 // Software pipeline over half groups of 13 samples: the loads of the next half are in flight
 // while the current half is processed (26 load registers, as for a whole-group batch, but no
 // wave waits a full memory latency per group). A whole group in flight ahead (52 registers, 2 waves
-// per SIMD) is +16 % at config 3 and flat at config 2 (profiles/r04_l_kbench_trig_deep_c*.json). body(group, u, raw) sees u = 0..25 in order;
-// roff advances by ngroups rows of 26. The last prefetch re-reads the current group (in bounds).
-template <class F>
-__device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, uint32_t& roff,
-                                           uint32_t row, F&& body) {
+// per SIMD) is +16 % at config 3 and flat at config 2 (profiles/r04_l_kbench_trig_deep_c*.json).
+// body(group, u, raw) sees u = 0..25 in order and half_end(group, h) runs after each half group
+// (h = 0, 1); rrow advances by ngroups rows of 26. The last prefetch re-reads the current group.
+template <class F, class E>
+__device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, uint32_t& rrow, uint32_t lane,
+                                           uint32_t row, F&& body, E&& half_end) {
     constexpr int H = kFirTaps / 2;
-    auto ld = [&](uint32_t off) { return *reinterpret_cast<const uint32_t*>(rbase + off); };
+    const __amdgpu_buffer_rsrc_t rs = raw_rsrc(rbase);
+    // the row offset is wave-uniform by construction; readfirstlane says so to the compiler, which
+    // otherwise may keep the loop counter in a VGPR and wrap every load in a waterfall loop
+    auto ld = [&](uint32_t off) {
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)lane, __builtin_amdgcn_readfirstlane((int)off), 0);
+    };
     uint32_t ra[H], rb[H];
     if (ngroups <= 0) return;
 #pragma unroll
-    for (int u = 0; u < H; ++u) ra[u] = ld(roff + (uint32_t)u * row);
+    for (int u = 0; u < H; ++u) ra[u] = ld(rrow + (uint32_t)u * row);
     for (int32_t g = 0; g < ngroups; ++g) {
 #pragma unroll
-        for (int u = 0; u < H; ++u) rb[u] = ld(roff + (uint32_t)(H + u) * row);
+        for (int u = 0; u < H; ++u) rb[u] = ld(rrow + (uint32_t)(H + u) * row);
 #pragma unroll
         for (int u = 0; u < H; ++u) body(g, u, ra[u]);
-        const uint32_t nxt = roff + (g + 1 < ngroups ? (uint32_t)kFirTaps * row : 0u);
+        half_end(g, 0);
+        const uint32_t nxt = rrow + (g + 1 < ngroups ? (uint32_t)kFirTaps * row : 0u);
 #pragma unroll
         for (int u = 0; u < H; ++u) ra[u] = ld(nxt + (uint32_t)u * row);
 #pragma unroll
         for (int u = 0; u < H; ++u) body(g, H + u, rb[u]);
-        roff += (uint32_t)kFirTaps * row;
+        half_end(g, 1);
+        rrow += (uint32_t)kFirTaps * row;
     }
+}
+template <class F>
+__device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, uint32_t& rrow, uint32_t lane,
+                                           uint32_t row, F&& body) {
+    run_groups(ngroups, rbase, rrow, lane, row, body, [](int32_t, int) {});
 }
 
 
@@ -178,8 +209,20 @@ struct Stepper<MKID_BASE_SVF, true> {
 #ifndef MKID_TRIG_MINW
 #define MKID_TRIG_MINW 3
 #endif
+// Issue priority falls with the wave's progress through its segment (done of ng groups): the
+// SIMD's older waves otherwise win every arbitration, finish first and leave the youngest to run
+// alone at a lone wave's issue rate. Priority 3 -> 2 -> 1 -> 0 at 70 / 85 / 95 % is -9 % k_trig_spec
+// at 1024 and 2048 channels, neutral at 256 (profiles/r04_p_*, r04_q_*).
+__device__ __forceinline__ void set_progress_prio(int32_t done, int32_t ng) {
+    const int32_t pc = done * 100;
+    if (pc >= 95 * ng) __builtin_amdgcn_s_setprio(0);
+    else if (pc >= 85 * ng) __builtin_amdgcn_s_setprio(1);
+    else if (pc >= 70 * ng) __builtin_amdgcn_s_setprio(2);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(TrigSpecArgs a) {
+    __builtin_amdgcn_s_setprio(3);
     const int64_t g = (int64_t)blockIdx.x * kSpecThreads + threadIdx.x;
     if (g >= (int64_t)a.C * a.nseg) return;
     const int C = a.C;
@@ -202,10 +245,16 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
     // all lanes of a wave share the segment (64 | C): a scalar row base and a 32-bit per-lane
     // offset give SGPR-base loads (no 64-bit address arithmetic per sample)
     const char* rbase = reinterpret_cast<const char*>(a.raw + (int64_t)__builtin_amdgcn_readfirstlane((int32_t)jw) * C);
-    uint32_t roff = (uint32_t)(c >> 1) * 4u;  // byte offset of the lane's dword (C even)
-    auto rload = [&](uint32_t off) { return *reinterpret_cast<const uint32_t*>(rbase + off); };
+    const uint32_t lane = (uint32_t)(c >> 1) * 4u;  // byte offset of the lane's dword (C even)
+    uint32_t rrow = 0;                              // wave-uniform byte offset of the current row
+    const __amdgpu_buffer_rsrc_t rs = raw_rsrc(rbase);
+    auto rload = [&](uint32_t off) {
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)lane, __builtin_amdgcn_readfirstlane((int)off), 0);
+    };
+    Lim16 lim{-32768, 32767};
+    asm volatile("" : "+v"(lim.lo), "+v"(lim.hi));
     QWin w0 = win;
-    const int32_t f0 = mf_q(w0, tp, 0, rload(roff));
+    const int32_t f0 = mf_q(w0, tp, 0, rload(0), lim);
     const TrigState st0 = jw == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
     auto body = [&](auto& sp) {
         // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0. A long
@@ -214,32 +263,36 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
         int32_t wbase = 0;
         if constexpr (MODE == MKID_BASE_SVF && std::is_same<std::decay_t<decltype(sp)>, Stepper<MODE, true>>::value) {
             wbase = (jw > 0 && wg > kFullWarm) ? wg - kFullWarm : 0;
-            run_groups(wbase, rbase, roff, (uint32_t)(2 * C),
-                       [&](int32_t, int u, uint32_t r) { sp.step_base(mf_q(win, tp, u, r)); });
+            run_groups(wbase, rbase, rrow, lane, (uint32_t)(2 * C),
+                       [&](int32_t, int u, uint32_t r) { sp.step_base(mf_q(win, tp, u, r, lim)); });
         }
-        run_groups(wg - wbase, rbase, roff, (uint32_t)(2 * C),
+        run_groups(wg - wbase, rbase, rrow, lane, (uint32_t)(2 * C),
                    [&](int32_t, int u, uint32_t r) {
                        EvInfo ev;
-                       (void)sp.step(mf_q(win, tp, u, r), ev);
+                       (void)sp.step(mf_q(win, tp, u, r, lim), ev);
                    });
         if (s > 0) a.s_spec[(int64_t)s * C + c] = sp.state();
         const int32_t len = (int32_t)(seg1 - seg0);
         const int32_t full = len - len % kFirTaps;
-        run_groups(__builtin_amdgcn_readfirstlane(full / kFirTaps), rbase, roff, (uint32_t)(2 * C),
+        const int32_t ng = __builtin_amdgcn_readfirstlane(full / kFirTaps);
+        run_groups(ng, rbase, rrow, lane, (uint32_t)(2 * C),
                    [&](int32_t gr, int u, uint32_t r) {
-                       const int32_t f = mf_q(win, tp, u, r);
+                       const int32_t f = mf_q(win, tp, u, r, lim);
                        EvInfo ev;
                        if (sp.step(f, ev)) {
                            if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gr * kFirTaps + u);
                            ++n;
                        }
+                   },
+                   [&](int32_t gr, int h) {
+                       if (h == 1) set_progress_prio(gr + 1, ng);
                    });
         const int32_t gi = full;
         const int32_t left = len - gi;  // tail < 26 samples, predicated
 #pragma unroll
         for (int u = 0; u < kFirTaps; ++u) {
             if (u < left) {
-                const int32_t f = mf_q(win, tp, u, rload(roff + (uint32_t)(2 * u * C)));
+                const int32_t f = mf_q(win, tp, u, rload(rrow + (uint32_t)(2 * u * C)), lim);
                 EvInfo ev;
                 if (sp.step(f, ev)) {
                     if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);

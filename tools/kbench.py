@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of libmkidgpu build variants in ONE process (cdna guide §5.4 rule 24).
 
-    python tools/kbench.py [--log2-samples 28] [--rounds 5] variantA.so variantB.so[:split] ...
+    python tools/kbench.py [--log2-samples 28] [--rounds 5] [--baseline svf] variantA.so variantB.so[:split] ...
 Each variant gets its own context on the same synthetic 1024-channel input (bench.py's feedline,
 calibrated); per round every variant processes the input once; per-kernel HIP-event times are
 reported as median / min over rounds.
@@ -24,9 +24,11 @@ def main():
     ap.add_argument('--log2-samples', type=int, default=28)
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--channels', type=int, default=1024)
+    ap.add_argument('--baseline', default='ema', choices=['ema', 'svf'])
     args = ap.parse_args()
     import torch
     import bench
+    from mkids_sdr_amd import _lib
     from mkids_sdr_amd import codecs, lut
     from mkids_sdr_amd.channelizer import Channelizer
 
@@ -94,6 +96,8 @@ def main():
         assert np.array_equal(np.asarray(dds['bins']) % N, np.asarray(feed['dds']['bins'])[perm] % N)
         ch.set_dds(dds['lut_i'], dds['lut_q'])
         ch.set_thresholds(np.full(C, -3000, np.int32))
+        if args.baseline == 'svf':   # bench.py's SVF settings (the EMA runs keep the context default)
+            ch.set_baseline(_lib.BASE_SVF, 41, 82, 93623, 8192)
         if env_set:
             del os.environ[env_set[0]]
         chans.append(ch)

@@ -58,7 +58,10 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=10)
-    p.add_argument('--warmup', type=int, default=2)
+    # the first launches of a fresh process run slower while the clock ramps (rocprofv3 traces,
+    # profiles/r04_v_*: config 3 k_front3 4.99, 4.65, 4.33, 4.30 ms then ~4.25; config 5 6.69 ->
+    # 5.45 over six launches): ten untimed steps reach the steady state of a continuous stream
+    p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--config', type=int, default=3, choices=sorted(CONFIGS))
     p.add_argument('--baseline', default='ema', choices=['ema', 'svf'])
     p.add_argument('--log2-samples', type=int, default=None, help='override the config sample count')

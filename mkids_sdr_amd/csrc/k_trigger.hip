@@ -128,28 +128,30 @@ __device__ __forceinline__ void run_groups(int32_t ngroups, const char* rbase, u
                                            uint32_t row, F&& body, E&& half_end) {
     constexpr int H = kFirTaps / 2;
     const __amdgpu_buffer_rsrc_t rs = raw_rsrc(rbase);
-    // the row offset is wave-uniform by construction; readfirstlane says so to the compiler, which
-    // otherwise may keep the loop counter in a VGPR and wrap every load in a waterfall loop
-    auto ld = [&](uint32_t off) {
-        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)lane, __builtin_amdgcn_readfirstlane((int)off), 0);
-    };
+    auto ld = [&](uint32_t off) { return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)lane, (int)off, 0); };
+    // the row offsets are wave-uniform by construction; one readfirstlane per half group says so
+    // to the compiler, which otherwise may keep them in VGPRs (a VALU add + readfirstlane per load,
+    // or, in the SVF warm-up, a waterfall loop around every load)
+    auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
     uint32_t ra[H], rb[H];
     if (ngroups <= 0) return;
+    rrow = uni(rrow);
 #pragma unroll
     for (int u = 0; u < H; ++u) ra[u] = ld(rrow + (uint32_t)u * row);
     for (int32_t g = 0; g < ngroups; ++g) {
+        const uint32_t cur = uni(rrow);
 #pragma unroll
-        for (int u = 0; u < H; ++u) rb[u] = ld(rrow + (uint32_t)(H + u) * row);
+        for (int u = 0; u < H; ++u) rb[u] = ld(cur + (uint32_t)(H + u) * row);
 #pragma unroll
         for (int u = 0; u < H; ++u) body(g, u, ra[u]);
         half_end(g, 0);
-        const uint32_t nxt = rrow + (g + 1 < ngroups ? (uint32_t)kFirTaps * row : 0u);
+        const uint32_t nxt = uni(cur + (g + 1 < ngroups ? (uint32_t)kFirTaps * row : 0u));
 #pragma unroll
         for (int u = 0; u < H; ++u) ra[u] = ld(nxt + (uint32_t)u * row);
 #pragma unroll
         for (int u = 0; u < H; ++u) body(g, H + u, rb[u]);
         half_end(g, 1);
-        rrow += (uint32_t)kFirTaps * row;
+        rrow = cur + (uint32_t)kFirTaps * row;
     }
 }
 template <class F>

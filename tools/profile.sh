@@ -15,7 +15,7 @@ export TMPDIR=/tmp
 cd /tmp
 B="python3 $ROOT/bench.py --no-cpu-baseline $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
-    -- $B --steps 10 --warmup 2 > "$OUT/kt.log" 2>&1
+    -- $B --steps 10 --warmup 10 > "$OUT/kt.log" 2>&1
 SMALL="--steps 1 --warmup 1"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
     -- $B $SMALL > "$OUT/fetch.log" 2>&1

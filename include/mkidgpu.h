@@ -276,6 +276,11 @@ int mkid_pulse_heights_counted(mkid_ctx* ctx, const float* d_phase, int64_t rows
 #define MKID_K_COPY 5         /* mkid_stream_copy (measured HBM roof)                     */
 #define MKID_K_HEIGHTS 6      /* mkid_pulse_heights                                       */
 #define MKID_K_COUNT 7
+/* enable: 0 off, 1 every kernel, or an OR of MKID_TIMING_ONLY(k): only those kernels. Each timed
+ * launch records two events on the stream, and an event record costs a few microseconds of
+ * stream time (rocprofv3 traces: 5-6 us gaps around timed kernels), so a throughput run times
+ * only the kernel it reports. Resets the accumulated times. */
+#define MKID_TIMING_ONLY(k) (2 << (k))
 int mkid_set_timing(mkid_ctx* ctx, int32_t enable);
 int mkid_get_timing(mkid_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches);
 const char* mkid_kernel_name(int32_t kernel);

@@ -242,8 +242,20 @@ class Channelizer:
         return out.cpu().numpy()
 
     # ---- timing ------------------------------------------------------------------------------
-    def set_timing(self, on):
-        self._chk(self._L.mkid_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on, kernels=None):
+        """on: time every kernel (HIP events); kernels: names (e.g. ['k_front']) to time only
+        those (mkid_set_timing with MKID_TIMING_ONLY masks; each timed launch costs two event
+        records on the stream)."""
+        if on and kernels:
+            names = [self._L.mkid_kernel_name(k).decode() for k in range(_lib.K_COUNT)]
+            mask = 0
+            for n in kernels:
+                if n not in names:
+                    raise ValueError('unknown kernel %r (one of %s)' % (n, names))
+                mask |= 2 << names.index(n)
+            self._chk(self._L.mkid_set_timing(self._h, mask))
+        else:
+            self._chk(self._L.mkid_set_timing(self._h, 1 if on else 0))
 
     def timing(self):
         out = {}

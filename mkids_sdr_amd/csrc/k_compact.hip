@@ -59,14 +59,15 @@ __global__ __launch_bounds__(kCmpThreads) void k_tile_sums(const int32_t* counts
     }
 }
 
-// d_counts[0] accumulates packets produced, d_counts[1] packets stored in `out` (<= cap), over
-// the sub-chunks of one process call (zeroed by the caller at the start of the call).
+// d_counts[0] = packets produced, d_counts[1] = packets stored in `out` (<= cap): written here,
+// once per process call (the call's single compaction covers all of its sub-chunks), so the
+// caller needs no zeroing launch.
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const int64_t* tile_kept, const int64_t* tile_raw,
                                                             int64_t ntiles, int64_t cap, int64_t* tile_off,
                                                             int64_t* d_counts) {
     __shared__ int64_t part[kScanThreads];
     __shared__ unsigned long long tot;
-    const int64_t prev = d_counts[1];
+    constexpr int64_t prev = 0;
     const int64_t per = (ntiles + kScanThreads - 1) / kScanThreads;
     const int64_t b = threadIdx.x * per;
     int64_t sum = 0, sumw = 0;
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const int64_t* tile_
     atomicAdd(&tot, (unsigned long long)sum);
     __syncthreads();
     if (threadIdx.x == 0) {
-        d_counts[0] += (int64_t)tot;
+        d_counts[0] = (int64_t)tot;
         const int64_t w = prev + part[kScanThreads - 1];
         d_counts[1] = w < cap ? w : cap;
     }
@@ -133,16 +134,33 @@ hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t 
 }
 
 // ---- history roll: dst[i] = concat(old[0:hist_rows], fresh[0:fresh_rows])[fresh_rows + i] ----
-__global__ void k_hist_roll(uint8_t* dst, const uint8_t* old_hist, const uint8_t* fresh,
-                            int64_t hist_rows, int64_t fresh_rows, int64_t row_bytes) {
+__device__ __forceinline__ void hist_roll_part(uint8_t* dst, const uint8_t* old_hist, const uint8_t* fresh,
+                                               int64_t hist_rows, int64_t fresh_rows, int64_t row_bytes,
+                                               int64_t first, int64_t stride) {
     const int64_t total = hist_rows * row_bytes;
-    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total;
-         b += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t b = first; b < total; b += stride) {
         const int64_t row = b / row_bytes, col = b % row_bytes;
         const int64_t src = fresh_rows + row;  // index into concat
         dst[b] = src < hist_rows ? old_hist[src * row_bytes + col]
                                  : fresh[(src - hist_rows) * row_bytes + col];
     }
+}
+
+__global__ void k_hist_roll(uint8_t* dst, const uint8_t* old_hist, const uint8_t* fresh,
+                            int64_t hist_rows, int64_t fresh_rows, int64_t row_bytes) {
+    hist_roll_part(dst, old_hist, fresh, hist_rows, fresh_rows, row_bytes,
+                   (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+}
+
+// two rolls in one launch (the call's trigger raw-phase and ADC histories): blocks [0, nb1) roll
+// job 1, the rest job 2 — one launch and one inter-kernel gap fewer per call
+__global__ void k_hist_roll2(RollJob j1, RollJob j2, int nb1) {
+    const bool first = (int)blockIdx.x < nb1;
+    const RollJob& j = first ? j1 : j2;
+    const int64_t b0 = first ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nb1;
+    const int64_t nb = first ? nb1 : (int64_t)gridDim.x - nb1;
+    hist_roll_part((uint8_t*)j.dst, (const uint8_t*)j.old_hist, (const uint8_t*)j.fresh, j.hist_rows,
+                   j.fresh_rows, j.row_bytes, b0 * blockDim.x + threadIdx.x, nb * blockDim.x);
 }
 
 hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
@@ -152,6 +170,17 @@ hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, 
     hipLaunchKernelGGL(k_hist_roll, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, (uint8_t*)dst,
                        (const uint8_t*)old_hist, (const uint8_t*)fresh, hist_rows, fresh_rows,
                        row_bytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_roll2(const RollJob& j1, const RollJob& j2, hipStream_t s) {
+    auto nblocks = [](const RollJob& j) {
+        const int64_t total = j.hist_rows * j.row_bytes;
+        const int64_t b = (total + 255) / 256;
+        return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+    };
+    const int nb1 = nblocks(j1), nb2 = nblocks(j2);
+    hipLaunchKernelGGL(k_hist_roll2, dim3(nb1 + nb2), dim3(256), 0, s, j1, j2, nb1);
     return hipGetLastError();
 }
 

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <utility>
 #include <atomic>
 #include <climits>
 #include <cmath>
@@ -123,6 +124,7 @@ struct mkid_ctx {
     uint64_t* d_ev_ws = nullptr;
     // timing
     bool timing = false;
+    uint32_t timing_mask = 0;   // bit k: kernel k is timed
     std::vector<KTime> pending;
     std::vector<hipEvent_t> pool;
     double tot_ms[MKID_K_COUNT] = {0};
@@ -157,7 +159,7 @@ static hipEvent_t get_event(mkid_ctx* c) {
 
 static void tstart(mkid_ctx* c, int k, KTime* kt, hipStream_t s) {
     kt->k = -1;
-    if (!c->timing) return;
+    if (!c->timing || !((c->timing_mask >> k) & 1u)) return;
     kt->a = get_event(c);
     kt->b = get_event(c);
     if (!kt->a || !kt->b) return;
@@ -612,7 +614,7 @@ static int plan_call(mkid_ctx* c, int64_t n, std::vector<SubPlan>& subs, int32_t
 // machine (speculative segments + fix-up) into segments seg_off.. of the call's slot table, then
 // the raw-phase history roll. Compaction (K8) runs once per call (compact_call).
 static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32_t stride, int32_t seg_off,
-                       int32_t capseg, hipStream_t s) {
+                       int32_t capseg, hipStream_t s, bool roll = true) {
     const int C = c->C;
     KTime kt;
     TrigSpecArgs ta{raw,        c->d_rhist, c->d_fir,   c->d_thr,      c->d_tstate,  c->d_tstate,
@@ -623,8 +625,13 @@ static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32
     tstart(c, MKID_K_TRIGGER, &kt, s);
     HIPCHK(c, launch_trigger(ta, s));
     tstop(c, &kt, s);
-    HIPCHK(c, launch_hist_roll(c->d_rtmp, c->d_rhist, raw, kRawHist, sp.J, (int64_t)C * 2, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_rhist, c->d_rtmp, (size_t)kRawHist * C * 2, hipMemcpyDeviceToDevice, s));
+    // the rolled history goes to the spare buffer and the two swap roles (enqueued kernels keep
+    // the pointers they were launched with): no device-to-device copy per call. roll = false:
+    // the caller rolls it together with the ADC history (raw_roll_job)
+    if (roll) {
+        HIPCHK(c, launch_hist_roll(c->d_rtmp, c->d_rhist, raw, kRawHist, sp.J, (int64_t)C * 2, s));
+        std::swap(c->d_rhist, c->d_rtmp);
+    }
     return MKID_OK;
 }
 
@@ -655,12 +662,12 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         int r = plan_call(c, n, subs, stride, capseg);
         if (r) return r;
     }
-    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, A));
     HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, A));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
     int32_t seg_off = 0;
     size_t si = 0;
+    RollJob last_roll{};
     for (int64_t off = 0; off < n; off += G, ++si) {
         const int64_t S = std::min<int64_t>(G, n - off);
         const int64_t K = S / M, J = S / N;
@@ -691,8 +698,12 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         HIPCHK(c, front4_supported(N) ? (c->front_variant == 5 ? launch_front5(fa, A) : launch_front4(fa, A))
                                       : (c->front_v2 ? launch_front2(N, fa, A) : launch_front(N, fa, A)));
         tstop(c, &kt, A);
-        int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, A);
+        const bool last = off + S >= n;
+        int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, A, !last);
         if (r) return r;
+        if (last) {
+            last_roll = RollJob{c->d_rtmp, c->d_rhist, raw, kRawHist, subs[si].J, (int64_t)C * 2};
+        }
         seg_off += subs[si].nseg;
         c->k0 += K;
         c->j0 += J;
@@ -704,8 +715,10 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         int r = compact_call(c, stride, capseg, d_events, cap, d_counts, A);
         if (r) return r;
     }
-    HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, c->H, n, 4, A));
-    HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)c->H * 4, hipMemcpyDeviceToDevice, A));
+    // the last sub-chunk's raw-phase history and the call's ADC history in one launch
+    HIPCHK(c, launch_hist_roll2(last_roll, RollJob{c->d_xtmp, c->d_xhist, x, c->H, n, 4}, A));
+    std::swap(c->d_rhist, c->d_rtmp);
+    std::swap(c->d_xhist, c->d_xtmp);
     c->iq_rows = c->iq_ch >= 0 ? n / N : 0;
     return MKID_OK;
 }
@@ -725,7 +738,6 @@ static int process_split(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     // B joins A's order (inputs written by earlier work on A, previous calls) ...
     HIPCHK(c, hipEventRecord(c->ev_start, A));
     HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
-    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, B));
     HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, B));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
@@ -758,7 +770,7 @@ static int process_split(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
             // carry the trailing 24 frames through d_zhist: always at the end of a call (next
             // call's history), and between sub-chunks too short to hold them
             HIPCHK(c, launch_hist_roll(c->d_ztmp, zprev, z, kLpfHist, K, (int64_t)C * 8, B));
-            HIPCHK(c, hipMemcpyAsync(c->d_zhist, c->d_ztmp, (size_t)kLpfHist * C * 8, hipMemcpyDeviceToDevice, B));
+            std::swap(c->d_zhist, c->d_ztmp);
             zprev = c->d_zhist;
             HIPCHK(c, hipEventRecord(c->ev_zfree[b], B));
         } else {
@@ -785,7 +797,7 @@ static int process_split(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     }
     // ADC history for the next call (all readers of d_xhist are channeliser launches on A)
     HIPCHK(c, launch_hist_roll(c->d_xtmp, c->d_xhist, x, H, n, 4, A));
-    HIPCHK(c, hipMemcpyAsync(c->d_xhist, c->d_xtmp, (size_t)H * 4, hipMemcpyDeviceToDevice, A));
+    std::swap(c->d_xhist, c->d_xtmp);
     // ... and A (the caller's stream) waits for everything B did
     HIPCHK(c, hipEventRecord(c->ev_done, B));
     HIPCHK(c, hipStreamWaitEvent(A, c->ev_done, 0));
@@ -826,7 +838,6 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
         int r = plan_call(c, rows * c->N, subs, stride, capseg);
         if (r) return r;
     }
-    HIPCHK(c, hipMemsetAsync(d_counts, 0, 16, s));
     int32_t seg_off = 0;
     int64_t r0 = 0;
     for (const SubPlan& sp : subs) {
@@ -1086,8 +1097,7 @@ static int pulse_heights(mkid_ctx* c, const float* d_phase, int64_t rows, int64_
     // keep the last H rows of (history, these rows) for the next call's early windows
     if (rows > 0) {
         HIPCHK(c, launch_hist_roll(c->d_phist_tmp, c->d_phist, d_phase, H, rows, (int64_t)c->C * 4, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->d_phist, c->d_phist_tmp, (size_t)H * c->C * 4, hipMemcpyDeviceToDevice,
-                                 c->stream));
+        std::swap(c->d_phist, c->d_phist_tmp);
         c->phist_rows = std::min<int64_t>(H, hrows + rows);
         c->phist_end = j0 + rows;
     }
@@ -1121,7 +1131,10 @@ int mkid_set_timing(mkid_ctx* c, int32_t enable) {
     if (!c) return MKID_E_ARG;
     int r = flush_timing(c);
     if (r) return r;
+    if (enable != 0 && enable != 1 && (enable & ~((MKID_TIMING_ONLY(MKID_K_COUNT - 1) << 1) - 2)) != 0)
+        FAIL(c, MKID_E_ARG, "timing: 0, 1 or an OR of MKID_TIMING_ONLY(k)");
     c->timing = enable != 0;
+    c->timing_mask = enable == 1 ? ((1u << MKID_K_COUNT) - 1u) : ((uint32_t)enable >> 1);
     for (int k = 0; k < MKID_K_COUNT; ++k) { c->tot_ms[k] = 0; c->launches[k] = 0; }
     return MKID_OK;
 }

@@ -152,6 +152,14 @@ hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t 
                           int64_t* scan_ws, hipStream_t s);
 hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
                             int64_t fresh_rows, int64_t row_bytes, hipStream_t s);
+// one history-roll job (k_hist_roll's arguments); launch_hist_roll2 runs two in one launch
+struct RollJob {
+    void* dst;
+    const void* old_hist;
+    const void* fresh;
+    int64_t hist_rows, fresh_rows, row_bytes;
+};
+hipError_t launch_hist_roll2(const RollJob& j1, const RollJob& j2, hipStream_t s);
 hipError_t launch_stream_copy(void* dst, const void* src, int64_t bytes, hipStream_t s);
 hipError_t launch_synth(int16_t* out, int64_t n, int64_t n0, const int16_t* base,
                         const mkid_synth_tone* tones, const mkid_pulse* pulses, int64_t npulses,

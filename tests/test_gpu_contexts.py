@@ -137,3 +137,45 @@ def test_adc_and_phase_streams_do_not_mix(gpu):
         ch.process(case.iq)
     finally:
         ch.close()
+
+
+def test_timing_mask_and_counts_written_per_call(gpu):
+    """mkid_set_timing with MKID_TIMING_ONLY masks times only the named kernels (bench.py's timed
+    steps record events around the front end alone); d_counts is written by each call's
+    compaction (no zeroing launch), so stale values in it do not leak into the next call."""
+    import torch
+    from mkids_sdr_amd import _lib
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 256, 1 << 20
+    case = signals.make_case(C, S, seed=51, pulses_per_ch=3.0, noise=100.0)
+    thr = quiet_thresholds(C, S // 4, 51)
+    x = torch.from_numpy(case.iq.reshape(-1)).to('cuda')
+    cap = 1 << 16
+    res = []
+    for junk in (0, 123456789):
+        ch = Channelizer(C, max_chunk=S)
+        try:
+            configure(ch, case, thr)
+            ev = torch.empty(cap, dtype=torch.int64, device='cuda')
+            cnt = torch.full((2,), junk, dtype=torch.int64, device='cuda')
+            ch.set_timing(True, kernels=['k_front'])
+            ch.process_device(x, S, None, ev, cap, cnt)
+            torch.cuda.synchronize()
+            t = ch.timing()
+            assert t['k_front'][1] == 1 and t['k_front'][0] > 0
+            assert t['k_trigger'][1] == 0 and t['k_compact'][1] == 0
+            ch.set_timing(True)
+            c = cnt.cpu().numpy().copy()
+            ch.process_device(x, S, None, ev, cap, cnt)
+            torch.cuda.synchronize()
+            t = ch.timing()
+            assert t['k_front'][1] == 1 and t['k_trigger'][1] == 1 and t['k_compact'][1] == 1
+            with pytest.raises(_lib.MkidError):   # bit 0 (every kernel) mixed with a mask
+                ch._chk(ch._L.mkid_set_timing(ch._h, 3))
+            with pytest.raises(ValueError):
+                ch.set_timing(True, kernels=['no_such_kernel'])
+            res.append((c, ev[:int(c[1])].cpu().numpy()))
+        finally:
+            ch.close()
+    assert res[0][0][0] > 0 and np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])

@@ -17,7 +17,11 @@
 // The result is bit-identical to the sequential oracle/trigger.c for every input; the speculation
 // only decides how much sequential work the fix-up does (EMA merges within ~10^2 samples on noisy
 // phase; the slow SVF baseline needs ~10^4, so its segments warm up over kSvfW, mkid_api.hip).
-// The 26-tap matched filter uses 24-bit multiply-adds (taps are 12-bit, samples 16-bit).
+// The 26-tap matched filter is 13 v_dot2_i32_i16 per sample in the walk (24-bit multiply-adds in
+// the fix-up's serial re-run). In SVF mode a pre-pass (k_mf_rows) writes the filtered rows once
+// and the walk reads them: its ~10^5-sample warm-up is bound by one wave's instruction stream,
+// and the filter was 16 of its 40 VALU per sample.
+#include <algorithm>
 #include <type_traits>
 
 #include "trig_common.h"
@@ -222,7 +226,10 @@ __device__ __forceinline__ void set_progress_prio(int32_t done, int32_t ng) {
     else if (pc >= 70 * ng) __builtin_amdgcn_s_setprio(2);
 }
 
-template <int MODE>
+// PRE: the rows hold the matched-filter output (a.filt, k_mf_rows) instead of the raw phase: the
+// walk takes f from the lane's half of the loaded dword (SVF mode, whose walk is bound by one
+// wave's instruction stream over a ~10^5-sample warm-up)
+template <int MODE, bool PRE = false>
 __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(TrigSpecArgs a) {
     __builtin_amdgcn_s_setprio(3);
     const int64_t g = (int64_t)blockIdx.x * kSpecThreads + threadIdx.x;
@@ -231,8 +238,11 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
     const int c = (int)(g % C);  // lanes of a wave = consecutive channels (coalesced raw loads)
     const int s = (int)(g / C);
     uint32_t tp[kFirTaps / 2];
+    if constexpr (!PRE) {
 #pragma unroll
-    for (int m = 0; m < kFirTaps / 2; ++m) tp[m] = pack2(a.fir[c * kFirTaps + 2 * m], a.fir[c * kFirTaps + 2 * m + 1]);
+        for (int m = 0; m < kFirTaps / 2; ++m)
+            tp[m] = pack2(a.fir[c * kFirTaps + 2 * m], a.fir[c * kFirTaps + 2 * m + 1]);
+    }
     const TrigCfg k{a.thr[c], MODE, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
     const int64_t seg0 = (int64_t)s * a.L;
     const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
@@ -240,13 +250,14 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
     // (exact); L and W are multiples of 26 whenever W > 0, so seg0 - jw is too
     const int64_t jw = (s == 0 || seg0 <= a.W) ? 0 : seg0 - a.W;
     QWin win;
-    load_qwin(win, a, c, jw);
+    if constexpr (!PRE) load_qwin(win, a, c, jw);
     const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
     uint64_t* slot = a.slots + sc * a.capseg;
     int32_t n = 0;
     // all lanes of a wave share the segment (64 | C): a scalar row base and a 32-bit per-lane
     // offset give SGPR-base loads (no 64-bit address arithmetic per sample)
-    const char* rbase = reinterpret_cast<const char*>(a.raw + (int64_t)__builtin_amdgcn_readfirstlane((int32_t)jw) * C);
+    const char* rbase = reinterpret_cast<const char*>((PRE ? a.filt : a.raw) +
+                                                      (int64_t)__builtin_amdgcn_readfirstlane((int32_t)jw) * C);
     const uint32_t lane = (uint32_t)(c >> 1) * 4u;  // byte offset of the lane's dword (C even)
     uint32_t rrow = 0;                              // wave-uniform byte offset of the current row
     const __amdgpu_buffer_rsrc_t rs = raw_rsrc(rbase);
@@ -255,8 +266,14 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
     };
     Lim16 lim{-32768, 32767};
     asm volatile("" : "+v"(lim.lo), "+v"(lim.hi));
+    const uint32_t half = (uint32_t)(c & 1) * 16u;   // PRE: the lane's int16 in the loaded dword
+    // filtered sample at ring position u from the loaded dword r
+    auto filt = [&](QWin& w, int u, uint32_t r) -> int32_t {
+        if constexpr (PRE) return __builtin_amdgcn_sbfe((int32_t)r, half, 16);
+        else return mf_q(w, tp, u, r, lim);
+    };
     QWin w0 = win;
-    const int32_t f0 = mf_q(w0, tp, 0, rload(0), lim);
+    const int32_t f0 = filt(w0, 0, rload(0));
     const TrigState st0 = jw == 0 ? a.st_in[c] : TrigState{0, 0, ST_REARM, 0, 0, 0, 0, 0, 0, 0};
     auto body = [&](auto& sp) {
         // warm-up: W is a multiple of 26 (host-checked), so the ring stays aligned at seg0. A long
@@ -266,12 +283,12 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
         if constexpr (MODE == MKID_BASE_SVF && std::is_same<std::decay_t<decltype(sp)>, Stepper<MODE, true>>::value) {
             wbase = (jw > 0 && wg > kFullWarm) ? wg - kFullWarm : 0;
             run_groups(wbase, rbase, rrow, lane, (uint32_t)(2 * C),
-                       [&](int32_t, int u, uint32_t r) { sp.step_base(mf_q(win, tp, u, r, lim)); });
+                       [&](int32_t, int u, uint32_t r) { sp.step_base(filt(win, u, r)); });
         }
         run_groups(wg - wbase, rbase, rrow, lane, (uint32_t)(2 * C),
                    [&](int32_t, int u, uint32_t r) {
                        EvInfo ev;
-                       (void)sp.step(mf_q(win, tp, u, r, lim), ev);
+                       (void)sp.step(filt(win, u, r), ev);
                    });
         if (s > 0) a.s_spec[(int64_t)s * C + c] = sp.state();
         const int32_t len = (int32_t)(seg1 - seg0);
@@ -279,7 +296,7 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
         const int32_t ng = __builtin_amdgcn_readfirstlane(full / kFirTaps);
         run_groups(ng, rbase, rrow, lane, (uint32_t)(2 * C),
                    [&](int32_t gr, int u, uint32_t r) {
-                       const int32_t f = mf_q(win, tp, u, r, lim);
+                       const int32_t f = filt(win, u, r);
                        EvInfo ev;
                        if (sp.step(f, ev)) {
                            if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gr * kFirTaps + u);
@@ -294,7 +311,7 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
 #pragma unroll
         for (int u = 0; u < kFirTaps; ++u) {
             if (u < left) {
-                const int32_t f = mf_q(win, tp, u, rload(rrow + (uint32_t)(2 * u * C)), lim);
+                const int32_t f = filt(win, u, rload(rrow + (uint32_t)(2 * u * C)));
                 EvInfo ev;
                 if (sp.step(f, ev)) {
                     if (n < a.capseg) slot[n] = make_packet(c, ev, f, a.j0 + seg0 + gi + u);
@@ -312,6 +329,53 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
         body(sp);
     }
     a.counts[sc] = n;
+}
+
+// Matched-filter pre-pass of the SVF path: f_j for rows [0, J) of every channel into a.filt
+// ([J][C] int16, the same Fix16_13 clamp as the walk's mf_q). Thread = (channel, block of
+// rows_per rows, a multiple of 26); the block's 25-row window is loaded first (raw history
+// before row 0, as in the walk). Loads and stores are buffer ops with wave-uniform row offsets.
+__global__ __launch_bounds__(kSpecThreads) void k_mf_rows(TrigSpecArgs a, int32_t rows_per) {
+    const int C = a.C;
+    const int64_t g = (int64_t)blockIdx.x * kSpecThreads + threadIdx.x;
+    const int c = (int)(g % C);
+    const int64_t j0 = (g / C) * (int64_t)rows_per;
+    if (j0 >= a.J) return;
+    const int64_t j1 = j0 + rows_per < a.J ? j0 + rows_per : a.J;
+    uint32_t tp[kFirTaps / 2];
+#pragma unroll
+    for (int m = 0; m < kFirTaps / 2; ++m) tp[m] = pack2(a.fir[c * kFirTaps + 2 * m], a.fir[c * kFirTaps + 2 * m + 1]);
+    QWin win;
+    load_qwin(win, a, c, j0);
+    const int64_t jr = __builtin_amdgcn_readfirstlane((int32_t)j0);
+    const char* rbase = reinterpret_cast<const char*>(a.raw + jr * C);
+    const __amdgpu_buffer_rsrc_t out = raw_rsrc(reinterpret_cast<const char*>(a.filt + jr * C));
+    const uint32_t lane = (uint32_t)(c >> 1) * 4u;
+    const uint32_t lane16 = (uint32_t)c * 2u;
+    const uint32_t row = (uint32_t)(2 * C);
+    Lim16 lim{-32768, 32767};
+    asm volatile("" : "+v"(lim.lo), "+v"(lim.hi));
+    auto put = [&](uint32_t roff, int32_t f) {
+        __builtin_amdgcn_raw_buffer_store_b16((unsigned short)f, out, (int)lane16,
+                                              __builtin_amdgcn_readfirstlane((int)roff), 0);
+    };
+    uint32_t rrow = 0;
+    const int32_t len = (int32_t)(j1 - j0);
+    const int32_t ng = __builtin_amdgcn_readfirstlane(len / kFirTaps);
+    run_groups(ng, rbase, rrow, lane, row, [&](int32_t gr, int u, uint32_t r) {
+        put((uint32_t)(gr * kFirTaps + u) * row, mf_q(win, tp, u, r, lim));
+    });
+    const int32_t left = len - ng * kFirTaps;   // tail < 26 rows (last block only), predicated
+    const __amdgpu_buffer_rsrc_t rs = raw_rsrc(rbase);
+#pragma unroll
+    for (int u = 0; u < kFirTaps; ++u) {
+        if (u < left) {
+            const uint32_t ro = rrow + (uint32_t)u * row;
+            const uint32_t r = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)lane,
+                                                                            __builtin_amdgcn_readfirstlane((int)ro), 0);
+            put(ro, mf_q(win, tp, u, r, lim));
+        }
+    }
 }
 
 // Re-run segment s of channel c from the true state T and the speculative state S0 side by side.
@@ -434,7 +498,18 @@ hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((threads + kSpecThreads - 1) / kSpecThreads));
     if (a.mode == MKID_BASE_EMA)
         hipLaunchKernelGGL(k_trig_spec<MKID_BASE_EMA>, grid, dim3(kSpecThreads), 0, s, a);
-    else if (a.mode == MKID_BASE_SVF)
+    else if (a.mode == MKID_BASE_SVF && a.filt) {
+        // filter pre-pass: row blocks of >= 520 rows (a multiple of 26), ~3 waves per SIMD
+        const int64_t nt = std::max<int64_t>(1, (int64_t)3072 * 64 / a.C);
+        int64_t rp = std::max<int64_t>(520, (a.J + nt - 1) / nt);
+        rp = (rp + kFirTaps - 1) / kFirTaps * kFirTaps;
+        const int64_t mthreads = (int64_t)a.C * ((a.J + rp - 1) / rp);
+        hipLaunchKernelGGL(k_mf_rows, dim3((unsigned)((mthreads + kSpecThreads - 1) / kSpecThreads)),
+                           dim3(kSpecThreads), 0, s, a, (int32_t)rp);
+        hipError_t e0 = hipGetLastError();
+        if (e0 != hipSuccess) return e0;
+        hipLaunchKernelGGL((k_trig_spec<MKID_BASE_SVF, true>), grid, dim3(kSpecThreads), 0, s, a);
+    } else if (a.mode == MKID_BASE_SVF)
         hipLaunchKernelGGL(k_trig_spec<MKID_BASE_SVF>, grid, dim3(kSpecThreads), 0, s, a);
     else
         hipLaunchKernelGGL(k_trig_spec<MKID_BASE_NONE>, grid, dim3(kSpecThreads), 0, s, a);

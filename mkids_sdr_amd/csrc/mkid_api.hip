@@ -84,6 +84,7 @@ struct mkid_ctx {
     // workspace
     float2* d_zb[2] = {nullptr, nullptr};
     int16_t* d_raw = nullptr;
+    int16_t* d_filt = nullptr;      // [Jmax][C] SVF filter pre-pass output (k_mf_rows)
     long long* d_ysum = nullptr;   // [C][2] fixed point 2^-kYsumFrac
     uint64_t* d_slots = nullptr;     // [C][nseg][capseg]
     int32_t* d_chcounts = nullptr;   // [C][nseg]
@@ -190,7 +191,7 @@ static int flush_timing(mkid_ctx* c) {
 static void free_all(mkid_ctx* c) {
     void* ptrs[] = {c->d_pfb,   c->d_pfbq,  c->d_bins,  c->d_lo,    c->d_fir,    c->d_ic,     c->d_qc,
                     c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
-                    c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_ysum, c->d_slots,
+                    c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_filt, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
                     c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff,
                     c->d_phist, c->d_phist_tmp, c->d_slot_ch};
@@ -573,6 +574,10 @@ int mkid_set_baseline(mkid_ctx* c, int32_t mode, int32_t alpha, int32_t kf, int3
     if (alpha < 0 || alpha > 1024) FAIL(c, MKID_E_ARG, "alpha must be Fix12_9 in 0..1024 (gain <= 2.0)");
     if (kf < 0 || kf >= (1 << 18) || kq < 0 || kq >= (1 << 18)) FAIL(c, MKID_E_ARG, "kf/kq must be Fix18_16");
     if (base_thr < 0 || base_thr > 65535) FAIL(c, MKID_E_ARG, "base_thr must be Fix16_13 (0..65535)");
+    if (mode == MKID_BASE_SVF && !c->d_filt) {   // the SVF filter pre-pass rows, allocated on first use
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, dalloc(&c->d_filt, (size_t)c->Jmax * c->C));
+    }
     c->mode = mode; c->alpha = alpha; c->kf = kf; c->kq = kq; c->base_thr = base_thr;
     return MKID_OK;
 }
@@ -621,7 +626,7 @@ static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32
                     c->d_sspec, c->d_send,  c->d_slots, c->d_chcounts, c->d_scratch, c->d_reruns,
                     sp.J,       c->j0,      C,          sp.nseg,       sp.L,         sp.W,
                     capseg,     c->mode,    c->alpha,   c->kf,         c->kq,        c->base_thr,
-                    c->cfg.dead_time, stride, seg_off};
+                    c->cfg.dead_time, stride, seg_off, c->d_filt};
     tstart(c, MKID_K_TRIGGER, &kt, s);
     HIPCHK(c, launch_trigger(ta, s));
     tstop(c, &kt, s);

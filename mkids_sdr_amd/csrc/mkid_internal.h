@@ -121,6 +121,9 @@ struct TrigSpecArgs {
     // the segments of one call's sub-chunks share one [C][seg_stride] slot table, so that a single
     // compaction at the end of the call orders packets channel-major over the whole call
     int32_t seg_stride, seg_off;
+    // [J][C] matched-filter output (int16) of the SVF path's filter pre-pass (k_mf_rows), so
+    // that the SVF walk, bound by one wave's instruction stream, skips the 26-tap filter
+    int16_t* filt = nullptr;
 };
 
 struct HeightArgs {

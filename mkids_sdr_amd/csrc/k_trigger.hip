@@ -212,8 +212,11 @@ struct Stepper<MKID_BASE_SVF, true> {
     __device__ __forceinline__ TrigState state() const { return from_fast_svf(fs); }
 };
 
+// 4 waves per SIMD (128 VGPRs; the occupancy also sizes the segments, mkid_plan.cpp): -4.4 %
+// k_trig_spec at 1024 channels and -5.4 % at 2048 against 3 waves (135 VGPRs), neutral at 256
+// (profiles/r04_ag_kbench_*.json); the few spilled dwords are outside the sample loops
 #ifndef MKID_TRIG_MINW
-#define MKID_TRIG_MINW 3
+#define MKID_TRIG_MINW 4
 #endif
 // Issue priority falls with the wave's progress through its segment (done of ng groups): the
 // SIMD's older waves otherwise win every arbitration, finish first and leave the youngest to run

@@ -84,6 +84,12 @@ def parse():
     p.add_argument('--launch-probe', action='store_true',
                    help='launcher check: each rank joins a gloo group, rank 0 prints the ranks\' '
                         'environment as one JSON line; no GPU call (CPU test of launch_ranks)')
+    p.add_argument('--atten-span', type=float, default=20.0,
+                   help='per-resonator attenuations uniform in [0, span] dB (define_DAC_LUT amplitudes)')
+    p.add_argument('--loop-ratio-min', type=float, default=0.1,
+                   help='IQ-loop radius / |centre| log-uniform in [min, 10]; 0: every loop centred at the origin')
+    p.add_argument('--witness-samples-log2', type=int, default=24,
+                   help='N > 1: samples of each rank\'s own feedline re-run for its parity witness')
     p.add_argument('--no-witness', action='store_true',
                    help='skip the parity witness: the one-core CPU sample (the first 2^cpu-samples-log2 '
                         'samples of the step input) re-run on the GPU from a reset context and compared '
@@ -91,9 +97,18 @@ def parse():
     return p.parse_args()
 
 
-def setup_feedline(C, fs, seed):
+def setup_feedline(C, fs, seed, atten_span=20.0, ratio_min=0.1):
     """Tones one per channel via the reference setup math (product host code, mkids_sdr_amd.lut):
-    DDS LUTs + bins (define_DDS_LUT / select_bins), DAC comb (define_DAC_LUT) -> ADC base."""
+    DDS LUTs + bins (define_DDS_LUT / select_bins), DAC comb (define_DAC_LUT) -> ADC base.
+
+    Operating conditions of the reference: per-resonator attenuations uniform
+    in [0, atten_span] dB, tone amplitudes 10^((atten_min - a)/20) inside one full-scale comb
+    (define_DAC_LUT, ROACH_Setup.py:499-502), and every tone behind a resonator IQ loop (iqsweep.RESDIFF
+    geometry, iqsweep.py:824-858) of radius R about a centre at 1 - R of the tone, R = ratio / (1 + ratio)
+    with loop radius / |centre| log-uniform in [ratio_min, 10] (a fifth of the loops centred at the
+    origin, R = 1). A photon moves the tone along its loop: the pulse amplitude of the synthetic source
+    is tone_amp * gain * R. The centres are loaded after the loop rotation (main(): rotateLoopsReady,
+    ROACH_Setup.py:645-667, then loadIQcenters, :595-617)."""
     from mkids_sdr_amd import lut
     N = 2 * C
     res = fs / lut.LUT_LEN
@@ -104,13 +119,32 @@ def setup_feedline(C, fs, seed):
     f_base = 4.0e9
     f_rf = [f_base + float((int(b) * upb + int(k)) * res) for b, k in zip(bins, m)]
     f_rf = [f - fs if f - f_base >= fs / 2 else f for f in f_rf]     # keep within +-fs/2 of LO
+    attens = rng.uniform(0.0, atten_span, C) if atten_span > 0 else np.zeros(C)
+    if ratio_min > 0:
+        ratio = np.exp(rng.uniform(np.log(ratio_min), np.log(10.0), C))
+        ratio[rng.random(C) < 0.2] = np.inf
+    else:
+        ratio = np.full(C, np.inf)
+    R = np.where(np.isfinite(ratio), ratio / (1.0 + np.where(np.isfinite(ratio), ratio, 0.0)), 1.0)
     dds = lut.define_dds_lut(f_rf, f_base, C, fs)
-    I_dac, Q_dac, freqs_dac, sf, phases = lut.define_dac_lut(f_rf, f_base, np.zeros(C), fs)
+    I_dac, Q_dac, freqs_dac, sf, phases = lut.define_dac_lut(f_rf, f_base, attens, fs)
     base = np.stack([I_dac, -Q_dac], axis=1).astype(np.int16)       # loop-back conjugation
     freq_index = np.array([int(round(((fs - f) % fs) / res)) for f in freqs_dac], np.int64)
     tone_amp = lut.FULL_SCALE / sf
+    gain = 10 ** ((attens.min() - attens) / 20.)
     return dict(dds=dds, base=base, freq_index=freq_index, phases=phases, tone_amp=tone_amp,
-                f_rf=f_rf, f_base=f_base)
+                f_rf=f_rf, f_base=f_base, attens=attens, gain=gain, loop_R=R)
+
+
+def resolve_backend(backend, world, device_count=None):
+    """--backend auto: RCCL when every rank has a GPU of its own (device_count() >= world, which does
+    not initialise the GPU), gloo otherwise (N ranks rehearsing on fewer GPUs)."""
+    if backend != 'auto':
+        return backend
+    if device_count is None:
+        import torch
+        device_count = torch.cuda.device_count()
+    return 'nccl' if device_count >= world else 'gloo'
 
 
 def make_pulses(C, n_samples, N, rate, rng):
@@ -291,8 +325,7 @@ def main():
     # device_count() does not initialise the GPU; ranks share a device only when there are more
     # ranks than GPUs (a one-GPU box rehearsing N > 1, gloo backend only: RCCL needs distinct GPUs)
     ndev = torch.cuda.device_count()
-    if args.backend == 'auto':
-        args.backend = 'nccl' if ndev >= world else 'gloo'
+    args.backend = resolve_backend(args.backend, world, ndev)
     gpu = local % max(ndev, 1)
     if world > 1 and args.backend == 'nccl' and world > ndev:
         raise SystemExit('%d ranks on %d GPUs: RCCL needs one GPU per rank (use --backend gloo)' % (world, ndev))
@@ -323,7 +356,7 @@ def main():
     S = 1 << log2
     J = S // N
     fs = cf['fs']
-    feed = setup_feedline(C, fs, 1000 + rank)
+    feed = setup_feedline(C, fs, 1000 + rank, args.atten_span, args.loop_ratio_min)
     mf = codecs.fir_quantise(np.loadtxt(os.path.join(ROOT, 'tests', 'golden', 'fir', 'matched_30us.txt')))
     lpf = codecs.fir_quantise(np.loadtxt(os.path.join(ROOT, 'tests', 'golden', 'fir',
                                                       'BlackmanFilter_250kHz.txt')))
@@ -346,7 +379,7 @@ def main():
     rng = np.random.default_rng(42 + rank)
     base = torch.from_numpy(feed['base']).to(dev)
     tones = np.zeros(C, dtype=[('amp', '<f4'), ('phase0', '<f4'), ('freq_index', '<i4'), ('pad', '<i4')])
-    tones['amp'] = feed['tone_amp']
+    tones['amp'] = feed['tone_amp'] * feed['gain'] * feed['loop_R']   # a photon moves the tone along its loop
     tones['phase0'] = -np.asarray(feed['phases'])
     tones['freq_index'] = feed['freq_index']
     d_tones = torch.from_numpy(tones.view(np.uint8)).to(dev)
@@ -377,6 +410,16 @@ def main():
     from mkids_sdr_amd import lut as _lut
     feed['dds'] = _lut.define_dds_lut(feed['f_rf'], feed['f_base'], C, fs, phase=np.arctan2(mq, mi))
     ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
+    # loadIQcenters (ROACH_Setup.py:595-617): the loop centre of each tone at 1 - R of its rotated
+    # rest IQ (the average IQ of the settled quiet stream)
+    ch.reset()
+    ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
+    ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
+    torch.cuda.synchronize(dev)
+    mi, mq = ch.avg_iq()
+    feed['ic'] = ((1.0 - feed['loop_R']) * mi).astype(np.float32)
+    feed['qc'] = ((1.0 - feed['loop_R']) * mq).astype(np.float32)
+    ch.set_centers(feed['ic'], feed['qc'])
     ch.reset()
     ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
     ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
@@ -468,6 +511,19 @@ def main():
                              (args.warmup + args.steps - 1) * J, ps, pt, N)
     reruns = ch.trigger_reruns()
     ch.set_timing(False)
+    # N > 1: every rank's own feedline gets a parity witness: the first
+    # 2^witness-samples-log2 samples of its step input re-run from a reset context, compared with
+    # the oracle in a CPU child pinned to a CPU of its own; rank 0 reports all ranks. Outside the
+    # timed region; the CPU throughput legs stay at N = 1.
+    parity_ranks = None
+    if world > 1 and not args.no_witness:
+        n_w = min(1 << args.witness_samples_log2, S)
+        wit_r = witness_device(ch, x, n_w, C, N, dev, heights is not None)
+        par_r = cpu_baseline(x, C, feed, lpf, mf, thr, n_w, n_w, base_mode, wit_r, witness_only=True,
+                             cpu=rank)
+        par_r = dict(par_r, rank=rank)
+        parity_ranks = [None] * world
+        dist.all_gather_object(parity_ranks, par_r, group=ctrl)
 
     if rank == 0:
         # measured HBM roof in the same run: stream copy of copy_mib MiB (the library's float4
@@ -588,6 +644,9 @@ def main():
         }
         if gather_info is not None:
             out['gather'] = gather_info
+        if parity_ranks is not None:
+            out['parity_ranks'] = parity_ranks
+            out['parity_ranks_green'] = all(p.get('green') for p in parity_ranks)
         if not args.no_cpu_baseline and world == 1:
             n1 = min(1 << args.cpu_samples_log2, S)
             wit = None
@@ -635,15 +694,16 @@ def witness_device(ch, x, n, C, N, dev, with_heights):
     return out
 
 
-def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall, mode, witness=None):
+def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall, mode, witness=None, witness_only=False, cpu=0):
     """The oracle (numpy float64 chain + C trigger, in the step's baseline mode) on a bounded
     sample of the same GPU input, timed by tools/cpu_baseline.py in a child process: (i) one
     pinned core, (ii) all usable cores chunk-parallel (cpu_baseline.kind = 'port'). `value` is the
     one-core rate. With `witness` (witness_device's arrays for the first n1 samples) the child
     also compares the oracle outputs of its one-core leg with them; the result comes back as
-    'parity'."""
+    'parity'. witness_only (N > 1, every rank): no timing legs, only the witness comparison of the
+    first n1 samples in a child pinned to CPU `cpu`; returns the 'parity' block."""
     from mkids_sdr_amd.pfb import pfb_prototype
-    n = max(n1, nall)
+    n = n1 if witness_only else max(n1, nall)
     n = min(n, x.numel() // 2)
     tmp = '/dev/shm' if os.path.isdir('/dev/shm') else '/tmp'
     inp = os.path.join(tmp, 'mkid_cpu_in_%d.npy' % os.getpid())
@@ -653,21 +713,28 @@ def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall, mode, witness=None):
         np.save(inp, x[:2 * n].view(-1, 2).cpu().numpy())
         np.savez(cfgp, C=C, pfb=pfb_prototype(2 * C), bins=feed['dds']['bins'], lut_i=feed['dds']['lut_i'],
                  lut_q=feed['dds']['lut_q'], lpf=lpf, fir=np.tile(mf, (C, 1)), thr=np.asarray(thr),
-                 mode=np.int64(mode))
+                 mode=np.int64(mode), ic=feed['ic'], qc=feed['qc'], attens=feed['attens'],
+                 loop_R=feed['loop_R'])
         cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--input', inp,
                '--cfg', cfgp, '--one-core-samples', str(min(n1, n)), '--all-core-samples', str(min(nall, n))]
         if witness is not None:
             np.savez(witp, **witness)
             cmd += ['--witness', witp]
+        if witness_only:
+            cmd += ['--witness-only', '--cpu', str(cpu)]
         del witness
         env = dict(os.environ)
         for k in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
             env[k] = '1'
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
         if r.returncode != 0:
+            if witness_only:
+                return {'green': False, 'error': 'witness child failed: %s' % r.stderr[-400:]}
             return {'value': None, 'unit': 'MSample/s', 'cores': 1, 'kind': 'port',
                     'sample': 'cpu baseline failed: %s' % r.stderr[-400:]}
         res = json.loads(r.stdout.strip().splitlines()[-1])
+        if witness_only:
+            return res['parity']
     finally:
         for p in (inp, cfgp, witp):
             try:

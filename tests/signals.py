@@ -22,15 +22,40 @@ class Case:
 
 def make_case(C, n_samples, fs=FS, n_tones=None, seed=0, noise=30.0, pulses_per_ch=0.0,
               amp_deg=(20.0, 100.0), tau_rise=0.1, tau_fall=65.0, window_phase=390,
-              pulse_margin=64, dds_phase=None):
+              pulse_margin=64, dds_phase=None, atten_db=None, loop_ratio=None):
     """Return a Case with .iq int16 [S][2] and every configuration array both sides need.
     dds_phase [C] (rad): per-channel DDS LUT phase, e.g. rotateLoopsReady's arctan2 of the
-    average IQ (ROACH_Setup.py:645-667); the tones and noise do not depend on it."""
+    average IQ (ROACH_Setup.py:645-667); the tones and noise do not depend on it.
+
+    atten_db [n_tones]: per-resonator attenuation (dB); tone amplitudes 10^((min - a)/20), the
+    rule of define_DAC_LUT (ROACH_Setup.py:499-502), then the comb is scaled to full scale as
+    freqCombLUT does (:451-461), so the strongest tone keeps the comb's level.
+
+    loop_ratio [n_tones] (or scalar): IQ-loop radius / |loop centre|. Each tone then passes a
+    resonator loop (geometry of iqsweep.RESDIFF, iqsweep.py:824-858: a circle of radius R about an
+    offset centre): at rest the tone sits at 1 (its DAC amplitude), the centre at 1 - R and a
+    photon moves it along the circle, tone (1 - R + R e^{i delta}), R = ratio / (1 + ratio). The
+    centres are then found and loaded the reference's way: the average IQ of a quiet,
+    noise-free run (the avgIQ accumulator) rotates the DDS (rotateLoopsReady, ROACH_Setup.py:
+    645-667) and ic + i qc = (1 - R) * the rotated rest IQ (findIQcenters / loadIQcenters,
+    :595-625). None = centre at the origin (R = 1), the round-1 cases."""
     N = 2 * C
     res = fs / LUT_LEN
     upb = LUT_LEN // N                       # fs/2^16 units per coarse bin
     rng = np.random.default_rng(seed)
     n_tones = C if n_tones is None else n_tones
+    if atten_db is None:
+        gain = np.ones(n_tones)
+    else:
+        atten_db = np.asarray(atten_db, np.float64)
+        gain = np.array([10 ** (+(atten_db.min() - a) / 20.) for a in atten_db])
+    if loop_ratio is None:
+        R = np.ones(n_tones)
+    else:
+        lr = np.broadcast_to(np.asarray(loop_ratio, np.float64), (n_tones,))
+        R = np.ones(n_tones)
+        fin = np.isfinite(lr)
+        R[fin] = lr[fin] / (1.0 + lr[fin])
     bins = rng.permutation(np.arange(1, N))[:n_tones]
     m = rng.integers(-(upb // 4), upb // 4 + 1, n_tones) if upb >= 4 else np.zeros(n_tones, int)
     f_dds = [float((int(b) * upb + int(k)) * res) for b, k in zip(bins, m)]
@@ -47,8 +72,7 @@ def make_case(C, n_samples, fs=FS, n_tones=None, seed=0, noise=30.0, pulses_per_
 
     # DAC side: tone at -f_dds (mod fs), freqCombLUT('yes') with the reference's random phases
     freqs_dac = [(fs - f) % fs for f in f_dds]
-    I_dac, Q_dac, sf, phases = setup_ref.freq_comb_lut('yes', freqs_dac, fs, res,
-                                                       [1.0] * n_tones)
+    I_dac, Q_dac, sf, phases = setup_ref.freq_comb_lut('yes', freqs_dac, fs, res, list(gain))
     base = np.stack([I_dac, -Q_dac], axis=1).astype(np.float64)   # loop-back conjugation
     tone_amp = setup_ref.FULL_SCALE / sf
     reps = -(-n_samples // LUT_LEN)
@@ -73,7 +97,7 @@ def make_case(C, n_samples, fs=FS, n_tones=None, seed=0, noise=30.0, pulses_per_
                 d = -A * (1 - np.exp(-tau / (tau_rise * N))) * np.exp(-tau / (tau_fall * N))
                 th = 2 * np.pi * ((int(round(f_dds[ch] / res)) * t[s0:e]) % LUT_LEN) / LUT_LEN \
                     - phases[ch]
-                z = tone_amp * np.exp(1j * th) * (np.exp(1j * d) - 1)
+                z = tone_amp * gain[ch] * R[ch] * np.exp(1j * th) * (np.exp(1j * d) - 1)
                 x[s0:e, 0] += z.real
                 x[s0:e, 1] += z.imag
     iq = np.clip(np.trunc(x), -32768, 32767).astype(np.int16)
@@ -81,6 +105,10 @@ def make_case(C, n_samples, fs=FS, n_tones=None, seed=0, noise=30.0, pulses_per_
     c = Case()
     c.C, c.N, c.fs, c.n_tones = C, N, fs, n_tones
     c.iq = iq
+    c.amps = np.zeros(C)
+    c.amps[:n_tones] = gain
+    c.loop_R = np.ones(C)
+    c.loop_R[:n_tones] = R
     c.bins = np.array(sel_bins, np.int64) % N
     c.lut_i, c.lut_q = lut_i, lut_q
     c.pfb = chain.pfb_prototype(N)
@@ -95,7 +123,30 @@ def make_case(C, n_samples, fs=FS, n_tones=None, seed=0, noise=30.0, pulses_per_
     c.phases = phases
     c.f_dds = f_dds
     c.pulses = pulse_list
+    c.resid = resid
+    if loop_ratio is not None:
+        _calibrate_loops(c, base, fs, res, dds_phase)
     return c
+
+
+def _calibrate_loops(c, base, fs, res, dds_phase):
+    """rotateLoopsReady + loadIQcenters on the noise-free, pulse-free comb (see make_case)."""
+    C, N = c.C, c.N
+    skip = 64                                 # rows of filter start-up
+    reps = max(2, -(-(skip + 64) * N // LUT_LEN))
+    quiet = np.clip(np.trunc(np.tile(base, (reps, 1))), -32768, 32767).astype(np.int16)
+    y = oracle_chain(c).process(quiet)['y'][skip:].mean(axis=0)
+    rot = np.angle(y) + (0. if dds_phase is None else np.asarray(dds_phase, np.float64))
+    for ch in range(C):
+        I, Q, _, _ = setup_ref.freq_comb_lut('no', [c.resid[ch]], fs / N * 2, res, [1.],
+                                             [float(rot[ch])], 'no')
+        c.lut_i[ch], c.lut_q[ch] = I, Q
+    c.dds_phase = rot
+    y_rot = oracle_chain(c).process(quiet)['y'][skip:].mean(axis=0)
+    cen = (1.0 - c.loop_R) * y_rot
+    c.ic = cen.real.astype(np.float32)
+    c.qc = cen.imag.astype(np.float32)
+    c.loop_radius = np.abs(y_rot) * c.loop_R  # |y - centre| at rest (y units)
 
 
 def _golden(rel):

@@ -74,6 +74,25 @@ def test_bench_gpus2_self_launch(gpu):
     assert min(g['last_step_counts']) > 1000
 
 
+def test_bench_gpus8_rehearsal(gpu):
+    """Config 4's protocol at its real rank count, on the one GPU: plain
+    `bench.py --gpus 8` (bench.py spawns the 8 ranks), gloo gather of 8 feedlines' packet lists to
+    rank 0 (the reference's 8 boards into one PacketMaster, PacketMaster.c:216-220, 589), and every
+    rank's parity witness (its own feedline's first 2^24 samples against the oracle, item 3)."""
+    out = _run_bench(['--gpus', '8', '--backend', 'gloo', '--check-gather', '--config', '3',
+                      '--log2-samples', '24', '--steps', '3', '--warmup', '1', '--no-cpu-baseline',
+                      '--copy-mib', '256'], timeout=280)
+    assert out['n_gpus'] == 8
+    g = out['gather']
+    assert g['backend'] == 'gloo' and g['ranks'] == 8
+    assert g['lists_equal_rank_own'] is True and g['feedlines_distinct'] is True
+    assert len(g['last_step_counts']) == 8 and min(g['last_step_counts']) > 100
+    pr = out['parity_ranks']
+    assert [p['rank'] for p in pr] == list(range(8))
+    assert out['parity_ranks_green'] is True, pr
+    assert all(p['samples'] == 1 << 24 and p['packets_equal_on_device_raw'] for p in pr)
+
+
 def test_bench_rccl_gather_world1(gpu):
     """The RCCL branch executed: init_process_group('nccl', device_id=...), the gloo control group,
     the device-buffer dist.gather on the side stream, the free-event hand-off, barrier + all_reduce

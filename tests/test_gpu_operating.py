@@ -1,0 +1,78 @@
+"""GPU parity under the reference's operating conditions: unequal per-resonator attenuation and
+off-origin IQ loop centres.
+
+The reference drives each resonator at its own attenuation — tone amplitudes 10^((atten_min - a)/20)
+(define_DAC_LUT, ROACH_Setup.py:499-502) inside one full-scale comb — and measures phase about the
+loop centre it loaded (loadIQcenters, ROACH_Setup.py:595-617; the host replay's
+atan2(Q - Qc, I - Ic), pulse_triggering_IQ.py:152) after rotating each loop (rotateLoopsReady,
+:645-667). signals.make_case reproduces that flow (per-tone attenuation, RESDIFF-style loops of
+radius R about a centre at 1 - R, DDS rotation, centres from the average IQ). Each case spreads its
+channels over an attenuation span (uniform in [0, span] dB) and over loop radius / |centre| ratios
+log-uniform in [0.1, 10] (a fifth of the channels centred at the origin).
+
+Bars: the same as tests/test_gpu_parity.py (phase within 1e-5 rad on every tone channel, Fix16_13
+within 1 LSB, packets bit-exact on the device's own phase, full-chain packets equal except
+downstream of a rounding flip).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import signals
+import test_gpu_parity as tp
+
+pytestmark = pytest.mark.gpu
+
+
+def operating_case(C, S, span, seed, pulses_per_ch):
+    rng = np.random.default_rng(1000 + seed)
+    att = rng.uniform(0.0, span, C)
+    ratio = np.exp(rng.uniform(np.log(0.1), np.log(10.0), C))
+    ratio[rng.random(C) < 0.2] = np.inf
+    kw = dict(seed=seed, atten_db=att, loop_ratio=ratio)
+    # 100-row pulse windows (the tail is at e^-1.5 there): the per-sample synthesis of 390-row
+    # windows dominates the suite's time at 2048 channels
+    case = signals.make_case(C, S, pulses_per_ch=pulses_per_ch, window_phase=100, **kw)
+    quiet = signals.make_case(C, min(S, 2 * C * 2048), pulses_per_ch=0, **kw)
+    thr = signals.thresholds_from_quiet(quiet, signals.oracle_chain(quiet).process(quiet.iq)['raw'])
+    case.ratio = ratio
+    return case, thr
+
+
+def _write_report(name, case, rep):
+    d = os.environ.get('MKID_PARITY_REPORT')
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    ymax = float(np.max(np.abs(case.loop_radius / case.loop_R)))
+    e, ymc = rep['err_rows'], rep['ymc']
+    settled = 16
+    with open(os.path.join(d, name + '.json'), 'w') as f:
+        json.dump({'C': case.C, 'rows': int(rep['rows']), 'amp': case.amps.tolist(),
+                   'loop_R': case.loop_R.tolist(), 'ymax': ymax,
+                   'radius_rel': (case.loop_radius / ymax).tolist(),
+                   'err': np.asarray(rep['err']).tolist(), 'flips': np.asarray(rep['flips']).tolist(),
+                   'err_settled': e[settled:].max(axis=0).tolist(),
+                   'argmax_row': e.argmax(axis=0).tolist(),
+                   'ymc_min': ymc.min(axis=0).tolist(), 'ymc_min_settled': ymc[settled:].min(axis=0).tolist(),
+                   'abs_iq_err': (e * ymc).max(axis=0).tolist(),
+                   'abs_iq_err_settled': (e[settled:] * ymc[settled:]).max(axis=0).tolist()}, f)
+
+
+@pytest.mark.parametrize('C,S,span,seed,splits', [
+    (256, 2 ** 18, 10.0, 61, [0, 2 ** 17 + 512, 2 ** 18]),
+    (256, 2 ** 18, 20.0, 62, None),
+    (1024, 2 ** 20, 10.0, 63, [0, 2 ** 19, 2 ** 20]),
+    (1024, 2 ** 20, 20.0, 64, None),
+    (2048, 2 ** 20, 20.0, 65, [0, 3 * 2 ** 17 + 4096, 2 ** 20]),
+])
+def test_operating_conditions(gpu, C, S, span, seed, splits):
+    case, thr = operating_case(C, S, span, seed, max(0.5, S / (2 * C) / 400))
+    rep = {}
+    try:
+        tp.compare(case, thr, splits or [0, S], report=rep)
+    finally:
+        if rep:
+            _write_report('operating_C%d_span%d' % (C, int(span)), case, rep)

@@ -64,3 +64,21 @@ def test_failed_rank_fails_the_launch():
     assert r.returncode == 3, r.stderr[-2000:]
     assert 'rank 1 exited with 3' in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+
+
+def test_backend_auto_resolution(monkeypatch):
+    """--backend auto: RCCL when device_count() >= world (one GPU per rank, the
+    driver's 8-GPU node), gloo when ranks must share a GPU (the one-GPU rehearsal); an explicit
+    backend is kept. device_count() is mocked: no GPU is touched."""
+    import torch
+    import bench
+    monkeypatch.setattr(torch.cuda, 'device_count', lambda: 8)
+    assert bench.resolve_backend('auto', 8) == 'nccl'
+    assert bench.resolve_backend('auto', 2) == 'nccl'
+    assert bench.resolve_backend('gloo', 8) == 'gloo'
+    monkeypatch.setattr(torch.cuda, 'device_count', lambda: 1)
+    assert bench.resolve_backend('auto', 8) == 'gloo'
+    assert bench.resolve_backend('auto', 2) == 'gloo'
+    assert bench.resolve_backend('auto', 1) == 'nccl'
+    assert bench.resolve_backend('nccl', 8) == 'nccl'
+    assert bench.resolve_backend('auto', 4, device_count=4) == 'nccl'

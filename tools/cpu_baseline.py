@@ -75,7 +75,8 @@ def run_chunk(args, collect=None):
     C = int(cfg['C'])
     N = 2 * C
     iq = np.load(inp, mmap_mode='r')
-    o = chain.OracleChain(C, cfg['pfb'], cfg['bins'], cfg['lut_i'], cfg['lut_q'], cfg['lpf'])
+    o = chain.OracleChain(C, cfg['pfb'], cfg['bins'], cfg['lut_i'], cfg['lut_q'], cfg['lpf'],
+                          cfg.get('ic'), cfg.get('qc'))
     tr = _trigger(trigger, cfg)
     p0 = max(0, a - prefix)
     t0 = time.perf_counter()
@@ -161,6 +162,22 @@ def witness_compare(col, witp, cfg):
                packets_equal_on_device_raw=bool(own_equal),
                channels_diverged_full_chain=len(diverged),
                channels_diverged_without_flip=len(unexplained))
+    if 'attens' in cfg:
+        # per-channel tone amplitude / loop columns: max phase error of the channels in each
+        # attenuation band and each loop radius / |centre| band
+        errc = err.max(axis=0)
+        att = np.asarray(cfg['attens'], np.float64)
+        R = np.asarray(cfg['loop_R'], np.float64)
+        ratio = np.where(R < 1.0, R / np.maximum(1.0 - R, 1e-12), np.inf)
+        out['by_atten_db'] = [dict(atten_db=[lo, hi], channels=int(m.sum()),
+                                   max_err_rad=float(errc[m].max()) if m.any() else None)
+                              for lo, hi in ((0, 5), (5, 10), (10, 15), (15, 20.001))
+                              for m in [(att >= lo) & (att < hi)]]
+        out['by_loop_ratio'] = [dict(ratio=[lo, hi], channels=int(m.sum()),
+                                     max_err_rad=float(errc[m].max()) if m.any() else None)
+                                for lo, hi in ((0.0, 0.3), (0.3, 1.0), (1.0, 10.0), (10.0, np.inf))
+                                for m in [(ratio >= lo) & (ratio < hi) if np.isfinite(hi) else ratio >= lo]]
+        out['by_loop_ratio'][-1]['ratio'] = [10.0, 'inf (centre at the origin)']
     green = (out['phase_max_err_rad'] <= 1e-5 and out['raw_max_abs_diff'] <= 1 and own_equal
              and not unexplained)
     if 'heights' in w.files:
@@ -212,6 +229,9 @@ def main():
                     help='0: every usable CPU (sched_getaffinity), capped at the cgroup CPU quota')
     ap.add_argument('--all-core-samples', type=int, required=True)
     ap.add_argument('--witness', default=None, help='.npz device outputs for the one-core sample')
+    ap.add_argument('--witness-only', action='store_true',
+                    help='N > 1 per-rank witness: only the oracle run + comparison of the one-core sample')
+    ap.add_argument('--cpu', type=int, default=0, help='--witness-only: index of the usable CPU to pin')
     ap.add_argument('--curve', default=None,
                     help='comma-separated worker counts: time only the chunk-parallel leg at each (the '
                          'cgroup cap is not applied), e.g. 4,8,16,32,64,256, and print one JSON line')
@@ -248,6 +268,13 @@ def main():
     # the same prefix, so their first rows' packets are approximate (a timing baseline only).
     prefix = (16 + 520) * N
 
+    if a.witness_only:
+        n1 = a.one_core_samples - a.one_core_samples % N
+        col = {}
+        run_chunk((aff[a.cpu % len(aff)], a.input, a.cfg, 0, n1, 0, 1 << 22), collect=col)
+        out['parity'] = witness_compare(col, a.witness, cfg)
+        print(json.dumps(out), flush=True)
+        return
     # (i) one core, one process
     n1 = a.one_core_samples - a.one_core_samples % N
     col = {} if a.witness else None

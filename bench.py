@@ -64,6 +64,9 @@ def parse():
     p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--config', type=int, default=3, choices=sorted(CONFIGS))
     p.add_argument('--baseline', default='ema', choices=['ema', 'svf'])
+    p.add_argument('--rearm-q8', type=int, default=None,
+                   help='trigger re-arm hysteresis /256 (mkid_set_rearm); default 32 for svf (removes the '
+                        'pulse-tail re-fires, tools/svf_characterize.py), 0 for ema')
     p.add_argument('--log2-samples', type=int, default=None, help='override the config sample count')
     p.add_argument('--pulse-rate', type=float, default=1.0 / 2048,
                    help='Poisson pulses per phase sample per channel')
@@ -374,6 +377,9 @@ def main():
     ch.set_lpf(lpf)
     ch.set_fir(np.tile(mf, (C, 1)))
     ch.set_baseline(base_mode, 41, 82, 93623, 8192)
+    if args.rearm_q8 is None:
+        args.rearm_q8 = 32 if args.baseline == 'svf' else 0
+    ch.set_rearm(args.rearm_q8)
 
     # ---- synthetic input resident in HBM ----
     rng = np.random.default_rng(42 + rank)
@@ -404,9 +410,11 @@ def main():
     d_events = torch.empty(cap, dtype=torch.int64, device=dev)
     d_counts = torch.zeros(2, dtype=torch.int64, device=dev)
     ch.set_thresholds(np.full(C, -(1 << 30), np.int32))
+    ch.set_accumulator(True)             # startAccumulator (ROACH_Setup.py:654-659)
     ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
     torch.cuda.synchronize(dev)
     mi, mq = ch.avg_iq()
+    ch.set_accumulator(False)
     from mkids_sdr_amd import lut as _lut
     feed['dds'] = _lut.define_dds_lut(feed['f_rf'], feed['f_base'], C, fs, phase=np.arctan2(mq, mi))
     ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
@@ -414,9 +422,11 @@ def main():
     # rest IQ (the average IQ of the settled quiet stream)
     ch.reset()
     ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
+    ch.set_accumulator(True)             # the settled second pass only
     ch.process_device(q, quiet_n, qphase, d_events, cap, d_counts)
     torch.cuda.synchronize(dev)
     mi, mq = ch.avg_iq()
+    ch.set_accumulator(False)            # off in the timed steps (the reference accumulates on demand)
     feed['ic'] = ((1.0 - feed['loop_R']) * mi).astype(np.float32)
     feed['qc'] = ((1.0 - feed['loop_R']) * mq).astype(np.float32)
     ch.set_centers(feed['ic'], feed['qc'])
@@ -520,7 +530,7 @@ def main():
         n_w = min(1 << args.witness_samples_log2, S)
         wit_r = witness_device(ch, x, n_w, C, N, dev, heights is not None)
         par_r = cpu_baseline(x, C, feed, lpf, mf, thr, n_w, n_w, base_mode, wit_r, witness_only=True,
-                             cpu=rank)
+                             cpu=rank, rearm_q8=args.rearm_q8)
         par_r = dict(par_r, rank=rank)
         parity_ranks = [None] * world
         dist.all_gather_object(parity_ranks, par_r, group=ctrl)
@@ -612,6 +622,8 @@ def main():
             'config': {'workload': '%s, 2^%d int16 I/Q samples per GPU per step' % (cf['name'], log2),
                        'config': args.config, 'channels': C, 'fft_len': N, 'pfb_taps': 4,
                        'fs': fs, 'samples_per_step_per_gpu': S, 'baseline': args.baseline,
+                       'rearm_q8': args.rearm_q8, 'atten_span_db': args.atten_span,
+                       'loop_ratio_min': args.loop_ratio_min,
                        'phase_materialised': not args.no_phase,
                        'pulse_heights_in_step': bool(cf['heights']),
                        'parallelism': 'feedline-per-GPU x%d%s' % (
@@ -653,7 +665,7 @@ def main():
             if not args.no_witness:
                 wit = witness_device(ch, x, n1, C, N, dev, heights is not None)
             out['cpu_baseline'] = cpu_baseline(x, C, feed, lpf, mf, thr, n1, 1 << args.cpu_all_samples_log2,
-                                               base_mode, wit)
+                                               base_mode, wit, rearm_q8=args.rearm_q8)
             par = out['cpu_baseline'].pop('parity', None)
             if par is not None:
                 out['parity'] = par
@@ -694,7 +706,8 @@ def witness_device(ch, x, n, C, N, dev, with_heights):
     return out
 
 
-def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall, mode, witness=None, witness_only=False, cpu=0):
+def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall, mode, witness=None, witness_only=False, cpu=0,
+                 rearm_q8=0):
     """The oracle (numpy float64 chain + C trigger, in the step's baseline mode) on a bounded
     sample of the same GPU input, timed by tools/cpu_baseline.py in a child process: (i) one
     pinned core, (ii) all usable cores chunk-parallel (cpu_baseline.kind = 'port'). `value` is the
@@ -713,7 +726,7 @@ def cpu_baseline(x, C, feed, lpf, mf, thr, n1, nall, mode, witness=None, witness
         np.save(inp, x[:2 * n].view(-1, 2).cpu().numpy())
         np.savez(cfgp, C=C, pfb=pfb_prototype(2 * C), bins=feed['dds']['bins'], lut_i=feed['dds']['lut_i'],
                  lut_q=feed['dds']['lut_q'], lpf=lpf, fir=np.tile(mf, (C, 1)), thr=np.asarray(thr),
-                 mode=np.int64(mode), ic=feed['ic'], qc=feed['qc'], attens=feed['attens'],
+                 mode=np.int64(mode), rearm_q8=np.int64(rearm_q8), ic=feed['ic'], qc=feed['qc'], attens=feed['attens'],
                  loop_R=feed['loop_R'])
         cmd = [sys.executable, os.path.join(ROOT, 'tools', 'cpu_baseline.py'), '--input', inp,
                '--cfg', cfgp, '--one-core-samples', str(min(n1, n)), '--all-core-samples', str(min(nall, n))]

@@ -68,7 +68,7 @@ typedef struct mkid_cfg {
     int32_t dds_entries;       /* P = 2^16 / C LO samples per channel; ROACH_Setup.py:521-530 */
     int32_t dead_time;         /* trigger dead time in phase samples (build decision)         */
     int32_t max_events_per_ch; /* per-call event capacity per channel (0 = derive from chunk) */
-    int32_t front;             /* MKID_FRONT_AUTO (fused K1-K6 kernel, N = 128..4096) or  
+    int32_t front;             /* MKID_FRONT_AUTO (fused K1-K6 kernel, N = 128..4096) or
                                   MKID_FRONT_SPLIT (channeliser + low-pass kernels, z in HBM)  */
     int64_t max_chunk;         /* largest nsamples per process call (workspace sizing)        */
     double sample_rate;        /* fs, complex S/s; ROACH_Setup.py:82                           */
@@ -98,7 +98,7 @@ int mkid_set_pfb(mkid_ctx* ctx, const float* coeffs, int32_t n);
 /* Host-only (no device needed): the effective taps h_q * 2^-S of mkid_set_pfb and S. */
 int mkid_pfb_effective_taps(const float* coeffs, int32_t T, int32_t N, float* out, int32_t* shift);
 /* Host-only: the channel order the N = 2048 front end (k_front3) gives its select threads for a
- * bin set (the C = 2048 order of the same scheme is reported too; k_front4 does not use it): out[st + (C/2) q] = channel read by thread st in instruction q.
+ * bin set (the C = 2048 order of the same scheme is reported too, unused by k_front5): out[st + (C/2) q] = channel read by thread st in instruction q.
  * Each wave keeps its own 128 channels; within them the order puts each half-wave's 32 Y reads on
  * distinct LDS bank pairs where the bins allow. A permutation of 0..C-1 (the identity for C other
  * than 1024 and 2048). Results do not depend on it: each channel's arithmetic is unchanged.
@@ -123,7 +123,10 @@ int mkid_set_lpf(mkid_ctx* ctx, const int16_t* taps12, int32_t ntaps);
 int mkid_set_fir(mkid_ctx* ctx, const int16_t* taps12, int32_t n_channels, int32_t ntaps);
 
 /* IQ loop centres [C] in channel-output units: replaces conv_phase_centers /
- * conv_phase_load_centers (ROACH_Setup.py:595-605). */
+ * conv_phase_load_centers (ROACH_Setup.py:595-605). phase = atan2(Q - qc, I - ic) is evaluated
+ * with the centre subtracted inside the low-pass (sum_i g_i (z_i - c/G) + r, G = sum of the
+ * low-pass taps, r the float64 residual of G c'), so the fp32 error of the phase does not grow
+ * with |centre| / loop radius. Centres must be finite. */
 int mkid_set_centers(mkid_ctx* ctx, const float* ic, const float* qc, int32_t n);
 
 /* Per-channel trigger thresholds [C], Fix16_13 raw units relative to baseline (negative-going):
@@ -134,6 +137,15 @@ int mkid_set_thresholds(mkid_ctx* ctx, const int32_t* thr, int32_t n);
  * kf/kq Fix18_16, base_thr Fix16_13 (0 = no gate). */
 int mkid_set_baseline(mkid_ctx* ctx, int32_t mode, int32_t alpha, int32_t kf, int32_t kq,
                       int32_t base_thr);
+
+/* Trigger re-arm hysteresis (K7 state machine, build decision: the firmware is absent): after its
+ * dead time a channel re-arms once e = f - baseline >= thr_c - floor(thr_c * frac_q8 / 256), i.e.
+ * at a level moved from its threshold toward the baseline by frac_q8 / 256 (0..256). 0 (the
+ * default) re-arms at the threshold, the round-1..4 rule, bit-identical. Without it a slow baseline
+ * (SVF) lets the pulse tail re-cross the threshold after the dead time; the
+ * reference's host replay holds off a fixed 1000 samples instead (pulse_triggering_v2.py:104-174).
+ * Kept across mkid_set_thresholds (the levels follow the thresholds). */
+int mkid_set_rearm(mkid_ctx* ctx, int32_t frac_q8);
 
 /* Forget all stream state (PFB/FIR history, baselines, trigger state, sample counter). */
 int mkid_reset_stream(mkid_ctx* ctx);
@@ -187,7 +199,15 @@ int mkid_read_iq_tap(mkid_ctx* ctx, int16_t* host_iq, int64_t cap_rows, int64_t*
  * re-run by the exact fix-up pass (0 = all speculation was right; results are exact either way). */
 int mkid_trigger_reruns(mkid_ctx* ctx, int64_t* total);
 
-/* Per-channel mean I/Q of the last processed call (avgIQ_bram, ROACH_Setup.py:654-662), [C] each. */
+/* avgIQ accumulator (K9): replaces startAccumulator / avgIQ_ctrl (ROACH_Setup.py:654-659,
+ * rotateLoopsReady). enable = 1 arms it — the sums restart (the avgIQ_ctrl strobe) and every
+ * following process call adds its rows; 0 stops it and keeps the sums. Off after mkid_create; the
+ * front ends skip the accumulation while it is off. mkid_reset_stream clears the sums and keeps
+ * the armed state. */
+int mkid_set_accumulator(mkid_ctx* ctx, int32_t enable);
+/* Per-channel mean I/Q (low-pass output y, ADC-count units) over the rows accumulated since the
+ * accumulator was last armed (avgIQ_bram, ROACH_Setup.py:654-662), [C] each. MKID_E_STATE when it
+ * holds no rows. */
 int mkid_avg_iq(mkid_ctx* ctx, float* mean_i, float* mean_q);
 
 /* Re-encode wide device packets as the reference 64-bit packet (host memory, C <= 254):
@@ -276,12 +296,14 @@ int mkid_pulse_heights_counted(mkid_ctx* ctx, const float* d_phase, int64_t rows
 #define MKID_K_COPY 5         /* mkid_stream_copy (measured HBM roof)                     */
 #define MKID_K_HEIGHTS 6      /* mkid_pulse_heights                                       */
 #define MKID_K_COUNT 7
-/* enable: 0 off, 1 every kernel, or an OR of MKID_TIMING_ONLY(k): only those kernels. Each timed
+/* mkid_set_timing: enable 0 off, any other value times every kernel (the round-1..3 meaning).
+ * mkid_set_timing_mask: an OR of MKID_TIMING_ONLY(k) times only those kernels (0 = off). Each timed
  * launch records two events on the stream, and an event record costs a few microseconds of
  * stream time (rocprofv3 traces: 5-6 us gaps around timed kernels), so a throughput run times
- * only the kernel it reports. Resets the accumulated times. */
-#define MKID_TIMING_ONLY(k) (2 << (k))
+ * only the kernel it reports. Both reset the accumulated times. */
+#define MKID_TIMING_ONLY(k) (1 << (k))
 int mkid_set_timing(mkid_ctx* ctx, int32_t enable);
+int mkid_set_timing_mask(mkid_ctx* ctx, uint32_t kernel_mask);
 int mkid_get_timing(mkid_ctx* ctx, int32_t kernel, double* total_ms, int64_t* launches);
 const char* mkid_kernel_name(int32_t kernel);
 

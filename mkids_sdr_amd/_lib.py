@@ -83,6 +83,7 @@ _SIGS = {
     'mkid_set_centers': [P, P, P, I32],
     'mkid_set_thresholds': [P, P, I32],
     'mkid_set_baseline': [P, I32, I32, I32, I32, I32],
+    'mkid_set_rearm': [P, I32],
     'mkid_reset_stream': [P],
     'mkid_process': [P, P, I64, P, P, I64, P],
     'mkid_process_device': [P, P, I64, P, P, I64, P],
@@ -91,10 +92,12 @@ _SIGS = {
     'mkid_read_raw_phase': [P, P, I64, P],
     'mkid_set_iq_tap': [P, I32],
     'mkid_read_iq_tap': [P, P, I64, P],
+    'mkid_set_accumulator': [P, I32],
     'mkid_avg_iq': [P, P, P],
     'mkid_trigger_reruns': [P, P],
     'mkid_pack_reference': [P, I64, P],
     'mkid_set_timing': [P, I32],
+    'mkid_set_timing_mask': [P, ctypes.c_uint32],
     'mkid_get_timing': [P, I32, P, P],
     'mkid_replay_trigger': [P, P, I64, I64, I32, P, P, I32, P],
     'mkid_make_template': [P, P, P, I64, P, P, P],

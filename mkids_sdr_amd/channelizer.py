@@ -112,6 +112,10 @@ class Channelizer:
         self._chk(self._L.mkid_set_baseline(self._h, int(mode), int(alpha), int(kf), int(kq),
                                             int(base_thr)))
 
+    def set_rearm(self, frac_q8):
+        """Trigger re-arm hysteresis (mkid_set_rearm): re-arm at thr - floor(thr * frac_q8 / 256)."""
+        self._chk(self._L.mkid_set_rearm(self._h, int(frac_q8)))
+
     def reset(self):
         self._chk(self._L.mkid_reset_stream(self._h))
 
@@ -187,7 +191,13 @@ class Channelizer:
         self._chk(self._L.mkid_trigger_reruns(self._h, ctypes.byref(n)))
         return n.value
 
+    def set_accumulator(self, on):
+        """startAccumulator (ROACH_Setup.py:654-659): True arms the avgIQ accumulator (the sums
+        restart; every following process call adds its rows), False stops it (sums kept)."""
+        self._chk(self._L.mkid_set_accumulator(self._h, 1 if on else 0))
+
     def avg_iq(self):
+        """Per-channel mean low-pass I/Q over the rows accumulated since set_accumulator(True)."""
         mi = np.empty(self.C, np.float32)
         mq = np.empty(self.C, np.float32)
         self._chk(self._L.mkid_avg_iq(self._h, _ptr(mi), _ptr(mq)))
@@ -252,8 +262,8 @@ class Channelizer:
             for n in kernels:
                 if n not in names:
                     raise ValueError('unknown kernel %r (one of %s)' % (n, names))
-                mask |= 2 << names.index(n)
-            self._chk(self._L.mkid_set_timing(self._h, mask))
+                mask |= 1 << names.index(n)
+            self._chk(self._L.mkid_set_timing_mask(self._h, mask))
         else:
             self._chk(self._L.mkid_set_timing(self._h, 1 if on else 0))
 

@@ -60,6 +60,16 @@ __device__ __forceinline__ float2 cmul_pk(float2 y, float2 t) {
     return float2_of(d);
 }
 
+// y * t + a (the DDC with the loop centre's -c' fused in: v_pk_fma_f32 in place of the
+// v_pk_mul_f32 of cmul_pk, no extra instruction)
+__device__ __forceinline__ float2 cmul_add_pk(float2 y, float2 t, float2 a) {
+    f2v d;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+        : "=&v"(d) : "v"(f2v_of(y)), "v"(f2v_of(t)), "v"(f2v_of(a)));
+    return float2_of(d);
+}
+
 // x + g * a with g one half of a uniform (SGPR) tap pair gp = (g_lo, g_hi): one v_pk_fma_f32
 // whose op_sel / op_sel_hi pick the same half of the pair for both lanes, so 13 pairs of
 // consecutive low-pass taps serve all 26 taps without duplicating any in SGPRs (the compiler

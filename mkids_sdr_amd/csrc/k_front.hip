@@ -1,4 +1,6 @@
-// Fused front end, K1-K6 in one pass over the ADC stream: polyphase filter bank + N-point FFT
+// Fused front end for N = 128 / 256 (configs[0]'s 64-channel geometry; N >= 512 runs the
+// wave-specialised k_front3 / k_front5, launch_fused below).
+// K1-K6 in one pass over the ADC stream: polyphase filter bank + N-point FFT
 // (2x oversampled, hop M = N/2) + bin select + DDC + 26-tap IQ low-pass decimating by 2 +
 // IQ-centre subtraction + atan2 + Fix16_13. The complex baseband z never leaves the CU: HBM sees
 // 4 B/sample of int16 I/Q in and 1 B/sample of raw phase (+2 B/sample float phase) out.
@@ -18,7 +20,8 @@
 //   LPF    transposed form, 13 complex accumulators per thread: frame 2j adds g_{2m+1} z to
 //          output j+m, frame 2j+1 adds g_{2m} z and completes output j:
 //          y_j = sum_i g_i z_{2j+1-i}      (taps int(lpf*(2**11-1))/2^11, ROACH_Pulses.py:69,88)
-//   phase  phi_j = atan2(Im y - qc, Re y - ic)     (pulse_triggering_IQ.py:152)
+//   phase  phi_j = atan2(Im y - qc, Re y - ic)     (pulse_triggering_IQ.py:152), accumulated
+//          centred: y - c = sum_i g_i (z_i - c') + r  (mkid_internal.h Centring)
 //          raw_j = clamp(rint(phi_j 2^13), +-25736) (Fix16_13, ROACH_Pulses.py:274-278)
 // Each run starts kLpfHist = 24 frames early (warm-up: the low-pass history is recomputed from
 // the ADC samples instead of being stored), so frames before the chunk come from an ADC history
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
 
     const int c = tid;  // channel of the select / low-pass / phase stage
     const int32_t bin = a.bins[c];
-    const float ic = a.ic[c], qc = a.qc[c];
+    const float2 ncen = a.cen.ncen[c], cor = a.cen.cor[c];   // centred low-pass (mkid_internal.h)
     // fused last pass for X[bin]: bin = jl + NSL s,
     //   X[bin] = sum_r W_RL^{r s} W_N^{jl r} Y[jl + r NSL]   (Stockham last pass, NS = NSL)
     constexpr int RL = G::RL, NSL = G::NSL;
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
             float2 X = yf[0];
 #pragma unroll
             for (int r = 1; r < RL; ++r) X = cmac(X, tl[r - 1], yf[r * NSL / 16 * 17]);
-            const float2 z = cmul(X, lov[f]);
+            const float2 z = cmul_add_pk(X, lov[f], ncen);   // z - c'
 #ifdef MKID_XP_STAMPS
             if (f == 0) {
                 asm volatile("" ::"v"(z.x), "v"(z.y));
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
                     const int jr = (kf - 1) >> 1;  // row within the run
                     ys.x += y.x;
                     ys.y += y.y;
-                    const float ph = phase_atan2(y.y - qc, y.x - ic);
+                    const float ph = phase_atan2(y.y + cor.y, y.x + cor.x);
                     int q = __float2int_rn(ph * 8192.0f);
                     q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
 #ifndef MKID_XP_STAMPS
@@ -335,8 +338,8 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
 #endif
                     __builtin_nontemporal_store((int16_t)q, raw_run + jr * C + c);
                     if (c == a.iq_ch && a.iqtap) {  // IQ snapshot tap (conv_phase_snapIQ_bram)
-                        a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y.x);
-                        a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y.y);
+                        a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y.x + a.cen.tap_off.x);
+                        a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y.y + a.cen.tap_off.y);
                     }
                 }
             }
@@ -347,7 +350,17 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     }
 }
 
-bool front_supported(int N) { return N == 128 || N == 256 || N == 512 || N == 1024 || N == 2048; }
+bool fused_supported(int N) { return N == 128 || N == 256 || N == 512 || N == 1024 || N == 2048 || N == 4096; }
+
+// the fused front end of each FFT length: k_front (this file) at N = 128 / 256, the
+// wave-specialised k_front3 at 512 / 1024 / 2048 and k_front5 at 4096 (round 5 retired k_front2
+// and k_front4: k_front3 measured -5.3 % at N = 512 and -10.7 % at N = 1024 against k_front2,
+// k_front5 -12.7 % against k_front4, same-box A/Bs in profiles/)
+hipError_t launch_fused(int N, const FrontArgs& a, hipStream_t s) {
+    if (N == 4096) return launch_front5(a, s);
+    if (N >= 512) return launch_front3(N, a, s);
+    return launch_front(N, a, s);
+}
 
 int64_t front_hist_samples(int N) { return (int64_t)(2 * kPfbTaps - 1 + kLpfHist) * (N / 2); }
 
@@ -373,9 +386,6 @@ hipError_t launch_front(int N, const FrontArgs& a, hipStream_t s) {
     switch (N) {
         case 128: return launch_front_n<128>(a, s);
         case 256: return launch_front_n<256>(a, s);
-        case 512: return launch_front_n<512>(a, s);
-        case 1024: return launch_front_n<1024>(a, s);
-        case 2048: return launch_front_n<2048>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

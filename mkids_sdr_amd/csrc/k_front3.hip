@@ -40,15 +40,16 @@ __device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
 // 768-thread workgroups per CU at one frame per iteration (k_front6, +25 %), commit ac8fe74.
 
 // Geometry per N. N = 2048 (config 3/4): 8 transform waves (4 sub-FFTs x 2 frames) + 8 select
-// waves (2 channels per thread), one workgroup per CU. N = 512 (config 2, round 4): 4 transform waves
-// (the 512-point FFT of each of 4 frames) + 4 select waves (1 channel per thread), two workgroups
-// per CU.
+// waves (2 channels per thread), one workgroup per CU. N = 1024 (round 5, replacing k_front2): 8
+// transform waves (2 sub-FFTs x 4 frames) + 8 select waves (1 channel per thread), one workgroup
+// per CU. N = 512 (config 2, round 4): 4 transform waves (the 512-point FFT of each of 4 frames) +
+// 4 select waves (1 channel per thread), two workgroups per CU.
 template <int N>
 struct G3 {
     static constexpr int NW = N / 512;                 // sub-FFTs per frame
     static constexpr int F = N == 2048 ? 2 : 4;        // frames per iteration
     static constexpr int FW = F * NW;                  // transform waves (one sub-FFT each)
-    static constexpr int SPT = N == 2048 ? 512 : 256;  // select threads
+    static constexpr int SPT = N == 512 ? 256 : 512;   // select threads
     static constexpr int BT = FW * 64 + SPT;
     static constexpr int M = N / 2, C = N / 2, T = kPfbTaps;
     static constexpr int CPT = C / SPT;                // channels per select thread
@@ -61,7 +62,7 @@ struct G3 {
     static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;
     static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
     static constexpr int WG_PER_CU = 16 * 64 / BT;     // 16 waves per CU
-    static_assert((N == 2048 || N == 512) && F * M == FW * 64 * 4 && C == SPT * CPT, "k_front3 geometry");
+    static_assert((N == 2048 || N == 1024 || N == 512) && F * M == FW * 64 * 4 && C == SPT * CPT, "k_front3 geometry");
     static_assert(lds_bytes * WG_PER_CU <= 160 * 1024, "LDS");
 };
 
@@ -71,6 +72,13 @@ template <int NW>
 __device__ __forceinline__ void ring3_put_nw(uint32_t* hop, int qoff, uint4 v) {
     if constexpr (NW == 4) {
         ring3_put(hop, qoff, v);
+    } else if constexpr (NW == 2) {
+        constexpr int Q = 256;
+        const int a = ring3_idx(qoff / 2);   // plane indices qoff / 2 and qoff / 2 + 1 (at a + 2)
+        hop[a] = v.x;
+        hop[Q + a] = v.y;
+        hop[a + 2] = v.z;
+        hop[Q + a + 2] = v.w;
     } else {
         static_assert(NW == 1, "ring layout");
         const int a = ring3_idx(qoff);
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
         const int st = rw * 64 + L;
         float2 tl[CPT][NW > 1 ? NW - 1 : 1];
         int yoff[CPT];
-        float ic[CPT], qc[CPT];
+        float2 ncen[CPT], cor[CPT];   // -c' and r of the centred low-pass (mkid_internal.h Centring)
         // channel of (thread, q): a host-chosen order (mkid_api.hip slot_order) that puts the 32
         // channels each half-wave reads per instruction on distinct LDS bank pairs of Y, each
         // wave keeping its own 128 channels (stores and LO loads stay within 2-4 lines)
@@ -257,8 +265,8 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
                 tl[q][u - 1] = make_float2((float)cs, (float)sn);
             }
             yoff[q] = yswz(bin & 511);
-            ic[q] = a.ic[c];
-            qc[q] = a.qc[c];
+            ncen[q] = a.cen.ncen[c];
+            cor[q] = a.cen.cor[c];
         }
         uint64_t gp[13];
 #pragma unroll
@@ -297,7 +305,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
                         float2 X = yf[yoff[q]];
 #pragma unroll
                         for (int u = 1; u < NW; ++u) X = cmac(X, tl[q][u - 1], yf[yoff[q] + u * G::REG]);
-                        z[q] = cmul_pk(X, lov[f][q]);
+                        z[q] = cmul_add_pk(X, lov[f][q], ncen[q]);   // z - c'
                     }
                     if ((f & 1) == 0) {
 #pragma unroll
@@ -321,7 +329,7 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
                                 const int c = cq[q];
                                 ys[q].x += y[q].x;
                                 ys[q].y += y[q].y;
-                                const float ph = phase_atan2(y[q].y - qc[q], y[q].x - ic[q]);
+                                const float ph = phase_atan2(y[q].y + cor[q].y, y[q].x + cor[q].x);
                                 int qv = __float2int_rn(ph * 8192.0f);
                                 qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
                                 // plain stores: with the slot order a wave's store covers its 64
@@ -331,8 +339,8 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
 #endif
                                 (raw_run + jr * C)[c] = (int16_t)qv;
                                 if (c == a.iq_ch && a.iqtap) {
-                                    a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y[q].x);
-                                    a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y[q].y);
+                                    a.iqtap[2 * ((k_b >> 1) + jr)] = iq16(y[q].x + a.cen.tap_off.x);
+                                    a.iqtap[2 * ((k_b >> 1) + jr) + 1] = iq16(y[q].y + a.cen.tap_off.y);
                                 }
                             }
                         }
@@ -370,6 +378,7 @@ static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
 hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s) {
     switch (N) {
         case 2048: return launch_front3_n<2048>(a, s);
+        case 1024: return launch_front3_n<1024>(a, s);
         case 512: return launch_front3_n<512>(a, s);
         default: return hipErrorInvalidValue;
     }

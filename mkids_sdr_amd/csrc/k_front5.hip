@@ -97,17 +97,12 @@ __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 
     p[4 * Q] = v1.x; p[5 * Q] = v1.y; p[6 * Q] = v1.z; p[7 * Q] = v1.w;
 }
 
-// element i of a uniform float array as a 32-bit lane offset from the (SGPR) base
-__device__ __forceinline__ float ldf(const float* base, int i) {
-    return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (uint32_t)i * 4u);
-}
-
 // measured and dropped (DESIGN.md §5 k_front5): T1 in registers, LO one frame ahead, one Horner
 // chain, even/odd chains, unsplit Y reads, no barrier between channels, transform-wave priority
 
 // select / DDC / low-pass / phase of CPT channels c0 + cs q per thread, frame k - 1 of iteration t
-// (the centres are re-read from global memory at each output frame and the avgIQ sums kept in LDS
-// ysl: registers go to the low-pass state)
+// (the centring constants -c' and r, mkid_internal.h Centring, are re-read from global memory with
+// the frame's LO row and the avgIQ sums kept in LDS ysl: registers go to the low-pass state)
 template <int CPT>
 __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0, int cs,
                                            int64_t k_b, int64_t k_start, int nrun, int nit) {
@@ -122,7 +117,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
         sincospi(-2.0 * (double)bin / G5::N, &sn, &cn);
         tb[q] = make_float2((float)cn, (float)sn);
         yoff[q] = yswz(bin & 511);
-        ysl[c] = make_float2(0.f, 0.f);
+        if (a.ysum) ysl[c] = make_float2(0.f, 0.f);
     }
     uint64_t gp[13];
 #pragma unroll
@@ -156,21 +151,23 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             const float2* yf = fbuf + f * G5::FB;
             // the LO row of this frame is loaded at the frame's start (loading it a frame ahead was
             // measured flat, DESIGN.md §5 k_front5); the centres of an output frame likewise
-            float2 lov[CPT];
+            float2 lov[CPT], ncv[CPT];
             {
                 const char* lorow = reinterpret_cast<const char*>(a.lo + ((lrow + f) & (a.P - 1)) * C);
-#pragma unroll
-                for (int q = 0; q < CPT; ++q) lov[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
-            }
-            [[maybe_unused]] float icv[CPT], qcv[CPT];
-            if (f == 1) {
+                const char* ncrow = reinterpret_cast<const char*>(a.cen.ncen);
 #pragma unroll
                 for (int q = 0; q < CPT; ++q) {
-                    icv[q] = ldf(a.ic, cb + cs * q);
-                    qcv[q] = ldf(a.qc, cb + cs * q);
+                    lov[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
+                    ncv[q] = *reinterpret_cast<const float2*>(ncrow + (uint32_t)(cb + cs * q) * 8u);
                 }
             }
-            auto zq = [&](int q) {
+            [[maybe_unused]] float2 corv[CPT];
+            if (f == 1) {
+                const char* corow = reinterpret_cast<const char*>(a.cen.cor);
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) corv[q] = *reinterpret_cast<const float2*>(corow + (uint32_t)(cb + cs * q) * 8u);
+            }
+            auto zq = [&](int q) {   // z - c' of channel slot q
                 const float2 lo = lov[q];
                 const float2* yq = yf + yoff[q];
                 // two 4-term Horner chains in W_N^{bin}, reads in two halves (8 VGPRs of reads in flight)
@@ -186,7 +183,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                 Xh = cmac(y4, Xh, tb[q]);
                 // joined by W_N^{4 bin} = (W_N^{bin})^4 (two squarings: a few ulp, far below the phase bar)
                 const float2 t2 = cmul_pk(tb[q], tb[q]);
-                return cmul_pk(cmac(Xl, Xh, cmul_pk(t2, t2)), lo);
+                return cmul_add_pk(cmac(Xl, Xh, cmul_pk(t2, t2)), lo, ncv[q]);
             };
             if (f == 0) {
 #pragma unroll
@@ -212,18 +209,23 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
 #pragma unroll
                     for (int m = 0; m < 12; ++m) acc[q][m] = fma_tap<0>(gp[m + 1], z, acc[q][m + 1]);  // g_{2m+2}
                     acc[q][12] = make_float2(0.f, 0.f);
-                    ph[q] = phase_atan2(y.y - qcv[q], y.x - icv[q]);
+                    ph[q] = phase_atan2(y.y + corv[q].y, y.x + corv[q].x);
                     if (out) {
                         const int c = cb + cs * q;
-                        // one owner per entry: a plain read-add-write (LDS float atomics ran at a small
-                        // fraction of the LDS rate and stalled every wave's LDS traffic on output frames)
-                        float2 ysv = ysl[c];
-                        ysv.x += y.x;
-                        ysv.y += y.y;
-                        ysl[c] = ysv;
+                        // avgIQ only while the accumulator is armed (mkid_set_accumulator; the
+                        // reference accumulates on demand, startAccumulator / avgIQ_ctrl,
+                        // ROACH_Setup.py:654-659). One owner per entry: a plain read-add-write (LDS
+                        // float atomics stalled every wave's LDS traffic on output frames)
+                        if (a.ysum) {
+                            float2 ysv = ysl[c];
+                            ysv.x += y.x;
+                            ysv.y += y.y;
+                            ysl[c] = ysv;
+                        }
                         if (a.iqtap) {               // uniform; the IQ-tap channel's sample by select
                             const bool hit = c == a.iq_ch;
-                            const uint32_t v = (uint32_t)(uint16_t)iq16(y.x) | ((uint32_t)(uint16_t)iq16(y.y) << 16);
+                            const float2 yt = make_float2(y.x + a.cen.tap_off.x, y.y + a.cen.tap_off.y);
+                            const uint32_t v = (uint32_t)(uint16_t)iq16(yt.x) | ((uint32_t)(uint16_t)iq16(yt.y) << 16);
                             iqv = hit ? v : iqv;
                             iqhit = iqhit || hit;
                         }

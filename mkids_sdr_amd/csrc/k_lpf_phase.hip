@@ -2,6 +2,7 @@
 // Fix16_13 quantisation.
 //   y_j = sum_i g_i z_{2j+1-i}                  (taps int(lpf*(2**11-1))/2^11, ROACH_Pulses.py:69,88)
 //   phi_j = atan2(Im y - qc, Re y - ic)          (pulse_triggering_IQ.py:152, conv_phase_centers)
+//   computed centred: y - c = sum_i g_i (z_i - c') + r  (mkid_internal.h Centring)
 //   raw_j = clamp(rint(phi_j * 2^13), +-25736)   (Fix16_13, ROACH_Pulses.py:274-278)
 // Thread = one channel x JB = 13*kLpfRounds consecutive outputs: a 26-deep register window slides
 // by 2 frames per output; slots are static inside each 13-output round, so z is read from HBM
@@ -21,7 +22,7 @@ __global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
     if (c >= a.C) return;
     const int64_t j0 = (int64_t)blockIdx.x * kLpfJB;
     const int C = a.C;
-    const float ic = a.ic[c], qc = a.qc[c];
+    const float2 ncen = a.cen.ncen[c], cor = a.cen.cor[c];   // centred low-pass (mkid_internal.h)
 
     // slot s holds frame f with (f - fbase) % 26 == s ; fbase = 2*j0 + 1 - 25
     float2 w[kFirTaps];
@@ -29,7 +30,8 @@ __global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
 #pragma unroll
     for (int i = 0; i < kFirTaps - 1; ++i) {
         const int64_t f = fbase + i;
-        w[i] = f >= 0 ? a.z[f * C + c] : a.zhist[(f + kLpfHist) * C + c];
+        const float2 v = f >= 0 ? a.z[f * C + c] : a.zhist[(f + kLpfHist) * C + c];
+        w[i] = make_float2(v.x + ncen.x, v.y + ncen.y);
     }
     float2 ys = make_float2(0.f, 0.f);
     for (int rd = 0; rd < kLpfRounds; ++rd) {
@@ -42,8 +44,12 @@ __global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
                 const int64_t f1 = 2 * j + 1;
                 const int s1 = (2 * u + kFirTaps - 1) % kFirTaps;  // slot of frame 2j+1
                 const int s0 = (2 * u + kFirTaps - 2) % kFirTaps;  // slot of frame 2j
-                if (u > 0 || rd > 0) w[s0] = a.z[(f1 - 1) * C + c];
-                w[s1] = a.z[f1 * C + c];
+                if (u > 0 || rd > 0) {
+                    const float2 v0 = a.z[(f1 - 1) * C + c];
+                    w[s0] = make_float2(v0.x + ncen.x, v0.y + ncen.y);
+                }
+                const float2 v1 = a.z[f1 * C + c];
+                w[s1] = make_float2(v1.x + ncen.x, v1.y + ncen.y);
                 float yr = 0.f, yi = 0.f;
 #pragma unroll
                 for (int i = 0; i < kFirTaps; ++i) {
@@ -53,14 +59,14 @@ __global__ __launch_bounds__(kLpfThreads) void k_lpf_phase(LpfArgs a) {
                 }
                 ys.x += yr;
                 ys.y += yi;
-                const float ph = phase_atan2(yi - qc, yr - ic);
+                const float ph = phase_atan2(yi + cor.y, yr + cor.x);
                 int q = __float2int_rn(ph * 8192.0f);
                 q = q < -25736 ? -25736 : (q > 25736 ? 25736 : q);
                 if (a.phase) a.phase[j * C + c] = ph;
                 a.raw[j * C + c] = (int16_t)q;
                 if (c == a.iq_ch && a.iqtap) {
-                    a.iqtap[2 * j] = iq16(yr);
-                    a.iqtap[2 * j + 1] = iq16(yi);
+                    a.iqtap[2 * j] = iq16(yr + a.cen.tap_off.x);
+                    a.iqtap[2 * j + 1] = iq16(yi + a.cen.tap_off.y);
                 }
             }
         }

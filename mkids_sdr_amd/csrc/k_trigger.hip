@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
         for (int m = 0; m < kFirTaps / 2; ++m)
             tp[m] = pack2(a.fir[c * kFirTaps + 2 * m], a.fir[c * kFirTaps + 2 * m + 1]);
     }
-    const TrigCfg k{a.thr[c], MODE, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
+    const TrigCfg k{a.thr[c], a.rearm[c], MODE, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
     const int64_t seg0 = (int64_t)s * a.L;
     const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
     // a segment closer than W to the sub-chunk start warms up from row 0 with the carried state
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
     int32_t tap[kFirTaps];
 #pragma unroll
     for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
-    const TrigCfg k{a.thr[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
+    const TrigCfg k{a.thr[c], a.rearm[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
     TrigState T{};
     bool override_ = false;  // T holds the true start state of segment s (from an unmerged re-run)
     int32_t reruns = 0;

@@ -59,8 +59,15 @@ struct mkid_ctx {
     int32_t* d_bins = nullptr;
     float2* d_lo = nullptr;
     int16_t* d_fir = nullptr;
-    float *d_ic = nullptr, *d_qc = nullptr;
+    // IQ-loop centres (loadIQcenters) and the centred low-pass constants derived from them and the
+    // low-pass taps (upload_centring): d_ncen = -c', d_cor = r (mkid_internal.h Centring)
+    std::vector<float> h_ic, h_qc;
+    float2 *d_ncen = nullptr, *d_cor = nullptr;
+    std::vector<double> h_gc;   // [2C] G c' (= r + c): added back to y' for the raw IQ
     int32_t* d_thr = nullptr;
+    int32_t* d_rearm = nullptr;      // [C] re-arm levels (upload_rearm)
+    std::vector<int32_t> h_thr;
+    int32_t rearm_q8 = 0;            // mkid_set_rearm hysteresis fraction (/256)
     LpfTaps lpf{};
     int32_t mode = MKID_BASE_EMA, alpha = 41, kf = 82, kq = 93623, base_thr = 8192;
     // stream state
@@ -77,15 +84,18 @@ struct mkid_ctx {
     int zi = 0;
     int64_t G = 0;  // pipeline sub-chunk (samples)
     int64_t last_raw_row = 0;       // first row of the last sub-chunk's raw phase in d_raw
-    bool fused = false;  // K1-K6 in one kernel (k_front / k_front2 / k_front4: no z buffers, no stream B work)
-    bool front_v2 = false;  // fused front end is k_front2 (N = 512..2048; MKID_FRONT_V1=1 forces v1)
-    int front_variant = 3;  // N = 512 / 2048: 3 = wave-specialised k_front3 (MKID_FRONT_V3=0: k_front2)
+    bool fused = false;  // K1-K6 in one kernel (k_front / k_front3 / k_front5: no z buffers, no stream B work)
     int64_t H = 0;       // ADC history samples carried between calls
     // workspace
     float2* d_zb[2] = {nullptr, nullptr};
     int16_t* d_raw = nullptr;
     int16_t* d_filt = nullptr;      // [Jmax][C] SVF filter pre-pass output (k_mf_rows)
-    long long* d_ysum = nullptr;   // [C][2] fixed point 2^-kYsumFrac
+    long long* d_ysum = nullptr;   // [C][2] fixed point 2^-kYsumFrac: sums of y' while armed
+    // avgIQ accumulator (K9; startAccumulator / avgIQ_ctrl, ROACH_Setup.py:654-659): armed by
+    // mkid_set_accumulator; rows accumulated since arming and the host-side sums of G c' over them
+    bool acc_on = false;
+    int64_t acc_rows = 0;
+    std::vector<double> acc_off;   // [2C]
     uint64_t* d_slots = nullptr;     // [C][nseg][capseg]
     int32_t* d_chcounts = nullptr;   // [C][nseg]
     int64_t* d_scan = nullptr;       // [C][nseg]
@@ -189,8 +199,8 @@ static int flush_timing(mkid_ctx* c) {
 }
 
 static void free_all(mkid_ctx* c) {
-    void* ptrs[] = {c->d_pfb,   c->d_pfbq,  c->d_bins,  c->d_lo,    c->d_fir,    c->d_ic,     c->d_qc,
-                    c->d_thr,   c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
+    void* ptrs[] = {c->d_pfb,   c->d_pfbq,  c->d_bins,  c->d_lo,    c->d_fir,    c->d_ncen,   c->d_cor,
+                    c->d_thr,   c->d_rearm, c->d_xhist, c->d_xtmp,  c->d_zhist,  c->d_ztmp,   c->d_rhist,
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_filt, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
                     c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff,
@@ -246,6 +256,7 @@ using plan::quantize_pfb;
 
 static int upload_lo_folded(mkid_ctx* c);
 static int upload_slot_order(mkid_ctx* c);
+static int upload_centring(mkid_ctx* c);
 static int upload_pfb(mkid_ctx* c, const float* coeffs);
 
 extern "C" {
@@ -286,17 +297,8 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     c->cfg = *cfg;
     c->device = device;
     c->C = C; c->N = N; c->M = N / 2; c->T = kPfbTaps; c->P = P;
-    c->fused = cfg->front == MKID_FRONT_AUTO && (front_supported(N) || front4_supported(N));
+    c->fused = cfg->front == MKID_FRONT_AUTO && fused_supported(N);
     {
-        const char* v1 = getenv("MKID_FRONT_V1");
-        c->front_v2 = c->fused && front2_supported(N) && !(v1 && atoi(v1) != 0);
-        const char* v3 = getenv("MKID_FRONT_V3");
-        c->front_variant = (v3 && atoi(v3) == 0) ? 2 : 3;
-
-        if (N == 4096) {
-            const char* v5 = getenv("MKID_FRONT_V5");
-            c->front_variant = (v5 && atoi(v5) == 0) ? 4 : 5;   // k_front5 unless MKID_FRONT_V5=0
-        }
         const char* so = getenv("MKID_SLOT_ORDER");
         c->slot_order_on = !(so && atoi(so) == 0);
     }
@@ -353,9 +355,10 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     AL(d_bins, C);
     AL(d_lo, (size_t)C * P);
     AL(d_fir, (size_t)C * kFirTaps);
-    AL(d_ic, C);
-    AL(d_qc, C);
+    AL(d_ncen, C);
+    AL(d_cor, C);
     AL(d_thr, C);
+    AL(d_rearm, C);
     AL(d_xhist, H);
     AL(d_xtmp, H);
     AL(d_zhist, (size_t)kLpfHist * C);
@@ -388,19 +391,22 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     for (int i = 0; i < C; ++i) bins[i] = i;
     std::vector<float2> lo((size_t)C * P, make_float2(32767.f / 32768.f, 0.f));
     std::vector<int16_t> fir((size_t)C * kFirTaps, 0);
-    std::vector<float> zero(C, 0.f);
     for (int i = 0; i < kFirTaps; ++i) c->lpf.g[i] = kBlackman250k[i] / 2048.0f;
+    c->h_thr = thr;
+    c->h_ic.assign(C, 0.f);
+    c->h_qc.assign(C, 0.f);
+    c->acc_off.assign(2 * (size_t)C, 0.0);
     if ((e = hipMemcpy(c->d_bins, bins.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_thr, thr.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_rearm, thr.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_lo, lo.data(), lo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_fir, fir.data(), fir.size() * 2, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_ic, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_qc, zero.data(), C * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        (e = hipMemcpy(c->d_fir, fir.data(), fir.size() * 2, hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "hipMemcpy defaults");
     c->h_lo = lo;
     c->h_bins = bins;
     *out = c;
-    if (upload_pfb(c, h.data()) != MKID_OK || upload_slot_order(c) != MKID_OK || mkid_reset_stream(c) != MKID_OK) {
+    if (upload_pfb(c, h.data()) != MKID_OK || upload_slot_order(c) != MKID_OK || upload_centring(c) != MKID_OK ||
+        mkid_reset_stream(c) != MKID_OK) {
         g_err = c->err;
         free_all(c);
         delete c;
@@ -543,7 +549,40 @@ int mkid_set_lpf(mkid_ctx* c, const int16_t* taps, int32_t n) {
     if (!c || !taps) return MKID_E_ARG;
     if (n != kFirTaps) FAIL(c, MKID_E_ARG, "low-pass must have 26 taps");
     for (int i = 0; i < n; ++i) c->lpf.g[i] = taps[i] / 2048.0f;
-    return MKID_OK;
+    return upload_centring(c);   // c' = c / G depends on the taps' sum G
+}
+
+// Centred low-pass constants (mkid_internal.h Centring): G = sum_i g_i (exact: g_i = k_i / 2^11),
+// c' = fp32(c / G), r = fp32(G c' - c) evaluated in float64 (G c' is exact there: 16 x 24 bits), so
+// y' + r = y - c up to the rounding of r (|r| ~ 2^-24 |c|). G = 0 (all taps zero): c' = 0, r = -c.
+static int upload_centring(mkid_ctx* c) {
+    double G = 0.0;
+    for (int i = 0; i < kFirTaps; ++i) G += (double)c->lpf.g[i];
+    std::vector<float2> nc((size_t)c->C), cr((size_t)c->C);
+    c->h_gc.assign(2 * (size_t)c->C, 0.0);
+    for (int ch = 0; ch < c->C; ++ch) {
+        const double ci = c->h_ic[ch], cq = c->h_qc[ch];
+        const float pi = G != 0.0 ? (float)(ci / G) : 0.f, pq = G != 0.0 ? (float)(cq / G) : 0.f;
+        nc[ch] = make_float2(-pi, -pq);
+        cr[ch] = make_float2((float)(G * pi - ci), (float)(G * pq - cq));
+        c->h_gc[2 * ch] = G * pi;
+        c->h_gc[2 * ch + 1] = G * pq;
+    }
+    int r = upload(c, c->d_ncen, nc.data(), nc.size() * 8);
+    return r ? r : upload(c, c->d_cor, cr.data(), cr.size() * 8);
+}
+
+// r + c of the IQ-tap channel (the tap reports y = y' + r + c)
+static float2 tap_offset(const mkid_ctx* c) {
+    if (c->iq_ch < 0) return make_float2(0.f, 0.f);
+    return make_float2((float)c->h_gc[2 * c->iq_ch], (float)c->h_gc[2 * c->iq_ch + 1]);
+}
+
+// the avgIQ accumulator after an armed call of J rows: the device summed y', the host adds J G c'
+static void acc_account(mkid_ctx* c, int64_t J) {
+    if (!c->acc_on) return;
+    c->acc_rows += J;
+    for (size_t i = 0; i < c->acc_off.size(); ++i) c->acc_off[i] += (double)J * c->h_gc[i];
 }
 
 int mkid_set_fir(mkid_ctx* c, const int16_t* taps, int32_t nch, int32_t nt) {
@@ -557,14 +596,34 @@ int mkid_set_fir(mkid_ctx* c, const int16_t* taps, int32_t nch, int32_t nt) {
 int mkid_set_centers(mkid_ctx* c, const float* ic, const float* qc, int32_t n) {
     if (!c || !ic || !qc) return MKID_E_ARG;
     if (n != c->C) FAIL(c, MKID_E_ARG, "need one centre per channel");
-    int r = upload(c, c->d_ic, ic, (size_t)n * 4);
-    return r ? r : upload(c, c->d_qc, qc, (size_t)n * 4);
+    for (int i = 0; i < n; ++i)
+        if (!std::isfinite(ic[i]) || !std::isfinite(qc[i])) FAIL(c, MKID_E_ARG, "centres must be finite");
+    c->h_ic.assign(ic, ic + n);
+    c->h_qc.assign(qc, qc + n);
+    return upload_centring(c);
+}
+
+// re-arm levels from the thresholds and the hysteresis fraction (plan::rearm_level)
+static int upload_rearm(mkid_ctx* c) {
+    std::vector<int32_t> lv(c->h_thr.size());
+    for (size_t i = 0; i < lv.size(); ++i) lv[i] = plan::rearm_level(c->h_thr[i], c->rearm_q8);
+    return upload(c, c->d_rearm, lv.data(), lv.size() * 4);
 }
 
 int mkid_set_thresholds(mkid_ctx* c, const int32_t* thr, int32_t n) {
     if (!c || !thr) return MKID_E_ARG;
     if (n != c->C) FAIL(c, MKID_E_ARG, "need one threshold per channel");
-    return upload(c, c->d_thr, thr, (size_t)n * 4);
+    int r = upload(c, c->d_thr, thr, (size_t)n * 4);
+    if (r) return r;
+    c->h_thr.assign(thr, thr + n);
+    return upload_rearm(c);
+}
+
+int mkid_set_rearm(mkid_ctx* c, int32_t frac_q8) {
+    if (!c) return MKID_E_ARG;
+    if (frac_q8 < 0 || frac_q8 > 256) FAIL(c, MKID_E_ARG, "re-arm fraction must be 0..256 (/256)");
+    c->rearm_q8 = frac_q8;
+    return upload_rearm(c);
 }
 
 int mkid_set_baseline(mkid_ctx* c, int32_t mode, int32_t alpha, int32_t kf, int32_t kq, int32_t base_thr) {
@@ -595,8 +654,10 @@ int mkid_reset_stream(mkid_ctx* c) {
                                  c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 16, c->stream));   // avgIQ: sums restart
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->acc_rows = 0;
+    std::fill(c->acc_off.begin(), c->acc_off.end(), 0.0);
     c->k0 = 0;
     c->j0 = 0;
     c->stream_kind = 0;
@@ -622,7 +683,7 @@ static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32
                        int32_t capseg, hipStream_t s, bool roll = true) {
     const int C = c->C;
     KTime kt;
-    TrigSpecArgs ta{raw,        c->d_rhist, c->d_fir,   c->d_thr,      c->d_tstate,  c->d_tstate,
+    TrigSpecArgs ta{raw,        c->d_rhist, c->d_fir,   c->d_thr,      c->d_rearm,   c->d_tstate,  c->d_tstate,
                     c->d_sspec, c->d_send,  c->d_slots, c->d_chcounts, c->d_scratch, c->d_reruns,
                     sp.J,       c->j0,      C,          sp.nseg,       sp.L,         sp.W,
                     capseg,     c->mode,    c->alpha,   c->kf,         c->kq,        c->base_thr,
@@ -667,12 +728,12 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         int r = plan_call(c, n, subs, stride, capseg);
         if (r) return r;
     }
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, A));
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
     int32_t seg_off = 0;
     size_t si = 0;
     RollJob last_roll{};
+    const Centring cen{c->d_ncen, c->d_cor, tap_offset(c)};
     for (int64_t off = 0; off < n; off += G, ++si) {
         const int64_t S = std::min<int64_t>(G, n - off);
         const int64_t K = S / M, J = S / N;
@@ -684,11 +745,10 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.pfbq = c->d_pfbq;
         fa.bins = c->d_bins;
         fa.lo = c->d_lo;
-        fa.ic = c->d_ic;
-        fa.qc = c->d_qc;
+        fa.cen = cen;
         fa.phase = d_phase ? d_phase + (off / N) * C : nullptr;
         fa.raw = raw;
-        fa.ysum = c->d_ysum;
+        fa.ysum = c->acc_on ? c->d_ysum : nullptr;
         fa.K = K;
         fa.k0 = c->k0;
         fa.avail = off;
@@ -697,11 +757,9 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.taps = c->lpf;
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
-        fa.variant = c->front_variant;
-        fa.slot_ch = c->N == 2048 ? c->d_slot_ch : nullptr;   // k_front3 only (k_front4: A/B lost)
+        fa.slot_ch = c->N == 2048 ? c->d_slot_ch : nullptr;   // k_front3 at N = 2048 only
         tstart(c, MKID_K_FRONT, &kt, A);
-        HIPCHK(c, front4_supported(N) ? (c->front_variant == 5 ? launch_front5(fa, A) : launch_front4(fa, A))
-                                      : (c->front_v2 ? launch_front2(N, fa, A) : launch_front(N, fa, A)));
+        HIPCHK(c, launch_fused(N, fa, A));
         tstop(c, &kt, A);
         const bool last = off + S >= n;
         int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, A, !last);
@@ -743,8 +801,8 @@ static int process_split(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
     // B joins A's order (inputs written by earlier work on A, previous calls) ...
     HIPCHK(c, hipEventRecord(c->ev_start, A));
     HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
-    HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)C * 16, B));
     const uint32_t* x = (const uint32_t*)d_iq;
+    const Centring cen{c->d_ncen, c->d_cor, tap_offset(c)};
     c->last_J = 0;
     int32_t seg_off = 0;
     size_t si = 0;
@@ -765,8 +823,8 @@ static int process_split(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
 
         // ---- stream B: low-pass + phase and trigger of this sub-chunk ----
         HIPCHK(c, hipStreamWaitEvent(B, c->ev_zready[b], 0));
-        LpfArgs la{z, zprev, c->d_ic, c->d_qc, d_phase ? d_phase + (off / N) * C : nullptr,
-                   c->d_raw, c->d_ysum, J, C, c->lpf,
+        LpfArgs la{z, zprev, cen, d_phase ? d_phase + (off / N) * C : nullptr,
+                   c->d_raw, c->acc_on ? c->d_ysum : nullptr, J, C, c->lpf,
                    c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr, c->iq_ch};
         tstart(c, MKID_K_FIR_PHASE, &kt, B);
         HIPCHK(c, launch_lpf_phase(la, B));
@@ -822,6 +880,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     HIPCHK(c, hipSetDevice(c->device));
     const int r = c->fused ? process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts)
                            : process_split(c, d_iq, n, d_phase, d_events, cap, d_counts);
+    if (r == MKID_OK) acc_account(c, n / c->N);
     // the context carries an ADC stream only once a call has been enqueued (a call that failed
     // before, e.g. in planning, leaves the stream kind as it was)
     if (r == MKID_OK) c->stream_kind = 1;
@@ -950,17 +1009,31 @@ int mkid_trigger_reruns(mkid_ctx* c, int64_t* total) {
     return MKID_OK;
 }
 
+int mkid_set_accumulator(mkid_ctx* c, int32_t enable) {
+    if (!c) return MKID_E_ARG;
+    if (enable != 0 && enable != 1) FAIL(c, MKID_E_ARG, "enable must be 0 or 1");
+    if (enable && !c->acc_on) {   // arming starts a new average (avgIQ_ctrl strobe + startAccumulator 1)
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 16, c->stream));
+        c->acc_rows = 0;
+        std::fill(c->acc_off.begin(), c->acc_off.end(), 0.0);
+    }
+    c->acc_on = enable != 0;
+    return MKID_OK;
+}
+
 int mkid_avg_iq(mkid_ctx* c, float* mi, float* mq) {
     if (!c || !mi || !mq) return MKID_E_ARG;
-    if (c->last_J <= 0) FAIL(c, MKID_E_STATE, "no data processed yet");
+    if (c->acc_rows <= 0)
+        FAIL(c, MKID_E_STATE, "the avgIQ accumulator holds no rows: arm it (mkid_set_accumulator) before processing");
     std::vector<long long> s(2 * (size_t)c->C);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(s.data(), c->d_ysum, (size_t)c->C * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const double scale = 1.0 / ((double)(1 << kYsumFrac) * (double)c->last_J);
+    const double inv = 1.0 / (double)c->acc_rows, scale = 1.0 / (double)(1 << kYsumFrac);
     for (int i = 0; i < c->C; ++i) {
-        mi[i] = (float)((double)s[2 * i] * scale);
-        mq[i] = (float)((double)s[2 * i + 1] * scale);
+        mi[i] = (float)(((double)s[2 * i] * scale + c->acc_off[2 * i]) * inv);
+        mq[i] = (float)(((double)s[2 * i + 1] * scale + c->acc_off[2 * i + 1]) * inv);
     }
     return MKID_OK;
 }
@@ -1132,16 +1205,19 @@ int mkid_stream_copy(mkid_ctx* c, void* d_dst, const void* d_src, int64_t bytes)
     return MKID_OK;
 }
 
-int mkid_set_timing(mkid_ctx* c, int32_t enable) {
+int mkid_set_timing_mask(mkid_ctx* c, uint32_t mask) {
     if (!c) return MKID_E_ARG;
+    if ((mask & ~((1u << MKID_K_COUNT) - 1u)) != 0) FAIL(c, MKID_E_ARG, "timing mask: an OR of MKID_TIMING_ONLY(k)");
     int r = flush_timing(c);
     if (r) return r;
-    if (enable != 0 && enable != 1 && (enable & ~((MKID_TIMING_ONLY(MKID_K_COUNT - 1) << 1) - 2)) != 0)
-        FAIL(c, MKID_E_ARG, "timing: 0, 1 or an OR of MKID_TIMING_ONLY(k)");
-    c->timing = enable != 0;
-    c->timing_mask = enable == 1 ? ((1u << MKID_K_COUNT) - 1u) : ((uint32_t)enable >> 1);
+    c->timing = mask != 0;
+    c->timing_mask = mask;
     for (int k = 0; k < MKID_K_COUNT; ++k) { c->tot_ms[k] = 0; c->launches[k] = 0; }
     return MKID_OK;
+}
+
+int mkid_set_timing(mkid_ctx* c, int32_t enable) {
+    return mkid_set_timing_mask(c, enable != 0 ? (1u << MKID_K_COUNT) - 1u : 0u);
 }
 
 int mkid_get_timing(mkid_ctx* c, int32_t k, double* total_ms, int64_t* launches) {

@@ -51,14 +51,24 @@ struct ChanArgs {
                             // older samples come from xhist
 };
 
+// Centred low-pass (K5-K6 with the IQ-loop centre c subtracted BEFORE the accumulation, DESIGN.md
+// §4): the kernels accumulate y' = sum_i g_i (z_i - c') with c' = c / G (G = sum_i g_i) and output
+// phase = atan2(y' + r), r = G c' - c (host, float64). The partial sums then stay at the loop's
+// radius instead of the tone's |y|, so the fp32 rounding of the accumulation no longer grows with
+// |c| / radius. y = y' + (r + c) where the raw IQ is needed (IQ tap: `tap_off`; avgIQ: the host).
+struct Centring {
+    const float2* ncen;     // [C] -c' (the DDC's fused add)
+    const float2* cor;      // [C] r
+    float2 tap_off;         // r + c of the IQ-tap channel
+};
+
 struct LpfArgs {
     const float2* z;        // [K][C]
     const float2* zhist;    // [24][C]
-    const float* ic;        // C
-    const float* qc;        // C
+    Centring cen;
     float* phase;           // [J][C] or nullptr
     int16_t* raw;           // [J][C]
-    long long* ysum;        // [C][2] per-channel sum of y (avgIQ), fixed point 2^-kYsumFrac, or nullptr
+    long long* ysum;        // [C][2] per-channel sum of y' (avgIQ), fixed point 2^-kYsumFrac, or nullptr
     int64_t J;
     int32_t C;
     LpfTaps taps;
@@ -83,11 +93,10 @@ struct FrontArgs {
     const uint2* pfbq;      // [N] int16 taps {h0|h1<<16, h2|h3<<16} of point p (scale 2^S in lo)
     const int32_t* bins;    // C
     const float2* lo;       // [P][C], conj(LUT)/2^15
-    const float* ic;        // C
-    const float* qc;        // C
+    Centring cen;
     float* phase;           // [K/2][C] or nullptr
     int16_t* raw;           // [K/2][C]
-    long long* ysum;        // [C][2] fixed point 2^-kYsumFrac, or nullptr
+    long long* ysum;        // [C][2] sums of y', fixed point 2^-kYsumFrac, or nullptr (accumulator off)
     int64_t K;              // frames in this chunk (even)
     int64_t k0;             // global index of the chunk's first frame
     int64_t frames_per_block;  // set by the launcher
@@ -97,7 +106,7 @@ struct FrontArgs {
     LpfTaps taps;
     int16_t* iqtap;         // [K/2][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
     int32_t iq_ch;
-    int32_t variant;        // N = 512 / 2048: 3 = wave-specialised k_front3, else k_front2; N = 4096: 5 = k_front5, else k_front4
+    int32_t pad;
     const int16_t* slot_ch; // [C] k_front3: channel of select slot st + 512 q (nullptr: identity)
 };
 
@@ -106,6 +115,7 @@ struct TrigSpecArgs {
     const int16_t* rhist;   // [25][C] previous call's last raw samples
     const int16_t* fir;     // [C][26] matched-filter taps (int12)
     const int32_t* thr;     // [C]
+    const int32_t* rearm;   // [C] re-arm levels (mkid_set_rearm; = thr without hysteresis)
     const TrigState* st_in; // [C] carried state (segment 0 starts from it)
     TrigState* st_out;      // [C] carried state after this call (may alias st_in)
     TrigState* s_spec;      // [nseg][C] speculative state at each segment start
@@ -194,13 +204,13 @@ inline hipError_t ensure_lds_attr(std::atomic<uint64_t>& mask, const void* fn, i
 }
 
 bool channelize_supported(int N);
-bool front_supported(int N);         // fused PFB..phase kernel available for this FFT length
-bool front2_supported(int N);        // the one-exchange fused kernel (k_front2.hip) for this N
-hipError_t launch_front2(int N, const FrontArgs& a, hipStream_t s);
-hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s);  // N = 512 / 2048, wave-specialised (k_front3.hip)
-bool front4_supported(int N);        // the 2048-channel fused kernel (k_front4.hip, N = 4096)
-hipError_t launch_front4(const FrontArgs& a, hipStream_t s);
-hipError_t launch_front5(const FrontArgs& a, hipStream_t s);  // N = 4096, wave-specialised (k_front5.hip)
+// fused PFB..phase front ends: k_front (N = 128 / 256), k_front3 (512 / 1024 / 2048, wave-
+// specialised), k_front5 (4096, wave-specialised); fused_supported / launch_fused dispatch by N
+bool fused_supported(int N);
+hipError_t launch_fused(int N, const FrontArgs& a, hipStream_t s);
+hipError_t launch_front(int N, const FrontArgs& a, hipStream_t s);   // N = 128 / 256 (k_front.hip)
+hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s);  // N = 512 / 1024 / 2048 (k_front3.hip)
+hipError_t launch_front5(const FrontArgs& a, hipStream_t s);         // N = 4096 (k_front5.hip)
 int64_t front_hist_samples(int N);  // ADC history the fused kernel reads before a chunk
 
 }  // namespace mkid

@@ -230,5 +230,11 @@ int pack_reference(const uint64_t* wide, int64_t n, uint64_t* out) {
     return 0;
 }
 
+int32_t rearm_level(int32_t thr, int32_t q8) {
+    const int64_t p = (int64_t)thr * q8;
+    const int64_t fl = p >= 0 ? p / 256 : -((-p + 255) / 256);   // floor(p / 256), no shift of a negative
+    return (int32_t)((int64_t)thr - fl);
+}
+
 }  // namespace plan
 }  // namespace mkid

@@ -78,6 +78,10 @@ void slot_order(const std::vector<int32_t>& bins, int C, std::vector<int16_t>& o
 // K1 taps as the device applies them: h_q = rint(h 2^S) int16, returns S
 int quantize_pfb(const float* h, int T, int N, std::vector<int16_t>& hq);
 
+// K7 re-arm level of a channel (mkid_set_rearm; oracle/trigger.py rearm_levels): the level moves
+// from the threshold toward 0 (the baseline) by q8 / 256: thr - floor(thr q8 / 256), q8 in 0..256
+int32_t rearm_level(int32_t thr, int32_t q8);
+
 // per-chunk channel-major packet lists concatenated -> one channel-major list (stable in time)
 void merge_channel_major(uint64_t* ev, int64_t n);
 

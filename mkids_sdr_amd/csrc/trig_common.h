@@ -8,7 +8,7 @@ namespace mkid {
 enum { ST_ARMED = 0, ST_PULSE = 1, ST_DEAD = 2, ST_REARM = 3 };
 
 struct TrigCfg {
-    int32_t thr, mode, alpha, kf, kq, base_thr, dead;
+    int32_t thr, rearm, mode, alpha, kf, kq, base_thr, dead;   // rearm: the channel's re-arm level
 };
 
 __device__ __forceinline__ int32_t tclamp16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
@@ -69,7 +69,7 @@ __device__ __forceinline__ bool trig_update(TrigState& s, int32_t f, const TrigC
     const int32_t cnt1 = s.cnt - 1;
     const bool to_pulse = armed && (e < k.thr);
     const bool to_rearm = dead && (cnt1 <= 0);
-    const bool to_armed = rearm && (e >= k.thr);
+    const bool to_armed = rearm && (e >= k.rearm);   // re-arm level (hysteresis; = thr without)
     ev = EvInfo{s.f2, s.f1, base_prev};
     s.cnt = emit ? k.dead : (dead ? cnt1 : s.cnt);
     s.st = to_pulse ? ST_PULSE : (emit ? ST_DEAD : (to_rearm ? ST_REARM : (to_armed ? ST_ARMED : s.st)));
@@ -84,7 +84,8 @@ __device__ __forceinline__ bool in_holdoff(const TrigState& s) { return !s.binit
 
 // Hot-loop form of trig_update for the EMA and no-baseline modes (k_trig_spec), same outputs:
 //  * the state machine is one code x: ARMED -1, PULSE -2, REARM 0, DEAD = dead-time samples
-//    left (>= 1). ARMED/REARM share one rule (x' = e < thr ? 2x : -1), DEAD counts down into
+//    left (>= 1). ARMED/REARM share one rule (x' = e < lv ? 2x : -1 with lv = thr in ARMED and the
+//    re-arm level in REARM), DEAD counts down into
 //    REARM, PULSE emits into DEAD max(dead, 1) (a DEAD count <= 0 behaves exactly like 1);
 //  * the baseline is already initialised (binit is settled once before the loop);
 //  * the dead-band gate |e| < base_thr is one unsigned compare (goff/glim), and alpha * e a
@@ -93,12 +94,12 @@ struct FastState {
     int32_t B, x, f1, f2;
 };
 struct FastCfg {
-    int32_t thr, alpha, dx;
+    int32_t thr, rearm, alpha, dx;
     uint32_t goff, glim;
 };
 
 __device__ __forceinline__ FastCfg fast_cfg(const TrigCfg& k) {
-    FastCfg q{k.thr, k.alpha, k.dead > 1 ? k.dead : 1, 0x80000000u, 0xffffffffu};
+    FastCfg q{k.thr, k.rearm, k.alpha, k.dead > 1 ? k.dead : 1, 0x80000000u, 0xffffffffu};
     if (k.base_thr > 0) {
         q.goff = (uint32_t)k.base_thr - 1u;
         q.glim = 2u * (uint32_t)k.base_thr - 1u;
@@ -128,7 +129,7 @@ __device__ __forceinline__ bool trig_update_fast(FastState& s, int32_t f, const 
     }
     const int32_t x = s.x;
     const bool emit = (x == -2) & (f > s.f1);
-    int32_t xn = e < k.thr ? 2 * x : -1;
+    int32_t xn = e < (x == 0 ? k.rearm : k.thr) ? 2 * x : -1;
     xn = x == -2 ? (f > s.f1 ? k.dx : -2) : xn;
     xn = x > 0 ? x - 1 : xn;
     s.x = xn;
@@ -194,7 +195,7 @@ __device__ __forceinline__ bool trig_update_svf(FastSvf& s, int32_t f, const Fas
     }
     const int32_t x = s.x;
     const bool emit = (x == -2) & (f > s.f1);
-    int32_t xn = e < k.thr ? 2 * x : -1;
+    int32_t xn = e < (x == 0 ? k.rearm : k.thr) ? 2 * x : -1;
     xn = x == -2 ? (f > s.f1 ? k.dx : -2) : xn;
     xn = x > 0 ? x - 1 : xn;
     s.x = xn;

@@ -295,9 +295,12 @@ class FpgaClient:
 
     def _read_avgiq(self, size):
         ch = self.sync()
+        ch.set_accumulator(False)
         self._process(ch, 64)                    # settle: filters forget the previous LO / LUTs
+        ch.set_accumulator(True)                 # startAccumulator 1 after the avgIQ_ctrl strobe
         self._process(ch, 256)                   # accumulate over 256 phase samples
         mi, mq = ch.avg_iq()
+        ch.set_accumulator(False)
         words = np.concatenate([np.rint(mi), np.rint(mq)]).astype('>i4')
         return words.tobytes()[:size]
 

@@ -7,7 +7,11 @@
  * 93623), baseline gate Fix16_13 (set_base_thresh.py:9-10 -> 8192); peak = 3-point parabolic fit
  * (Utils/bin.py:12-16) in integer arithmetic; packet fields Fix12_9 offset-binary
  * (ROACH_Pulses.py:852-859, Utils/bin.py:5-7). The state machine (edge trigger, peak on the first
- * upturn, dead time, re-arm above threshold) is a build decision: the firmware is absent.
+ * upturn, dead time, re-arm at the re-arm level) is a build decision: the firmware is absent.
+ * Re-arm level (round 5, hysteresis): a channel re-arms after its dead time once e >= rearm[c];
+ * rearm = thr (NULL) is the round-1..4 rule. mkid_set_rearm derives the levels from the thresholds
+ * (oracle/trigger.py rearm_levels); the reference's own host replay re-arms only after a fixed
+ * 1000-sample skip (pulse_triggering_v2.py:104-174).
  *
  * Semantics shared bit-for-bit with mkids_sdr_amd/csrc/k_trigger.hip and oracle/trigger_ref.py.
  */
@@ -55,15 +59,16 @@ void oracle_trig_reset_state(trig_state* st, int32_t C) {
 }
 
 /* raw: [J][C] int16 Fix16_13 time-major; hist: [25][C] previous raw (hist[24] = newest);
- * taps: [C][26] int12; st: [C]. Events are written channel-major, time-ascending; returns the
+ * taps: [C][26] int12; st: [C]; rearm: [C] re-arm levels or NULL (= thr). Events are written channel-major, time-ascending; returns the
  * total number produced (may exceed cap; only cap are written). counts[c] (nullable) = per-ch. */
 int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* taps,
-                       const int32_t* thr, int32_t mode, int32_t alpha, int32_t kf, int32_t kq,
+                       const int32_t* thr, const int32_t* rearm, int32_t mode, int32_t alpha, int32_t kf, int32_t kq,
                        int32_t base_thr, int32_t dead, int16_t* hist, trig_state* st, int64_t j0,
                        uint64_t* ev, int64_t cap, int64_t* counts) {
     int64_t total = 0;
     for (int32_t c = 0; c < C; ++c) {
         trig_state s = st[c];
+        const int32_t lvl = rearm ? rearm[c] : thr[c];
         int64_t nc = 0;
         for (int64_t j = 0; j < J; ++j) {
             int32_t acc = 0;
@@ -108,7 +113,7 @@ int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* 
                     if (s.cnt <= 0) s.st = ST_REARM;
                     break;
                 default:
-                    if (e >= thr[c]) s.st = ST_ARMED;
+                    if (e >= lvl) s.st = ST_ARMED;
                     break;
             }
             s.f2 = s.f1;

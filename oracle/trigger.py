@@ -27,7 +27,7 @@ def lib():
         L = ctypes.CDLL(_SO)
         P = ctypes.c_void_p
         L.oracle_trigger.restype = ctypes.c_int64
-        L.oracle_trigger.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, P, ctypes.c_int32,
+        L.oracle_trigger.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, P, P, ctypes.c_int32,
                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.c_int32, ctypes.c_int32, P, P, ctypes.c_int64, P,
                                      ctypes.c_int64, P]
@@ -43,14 +43,23 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def rearm_levels(thr, frac_q8):
+    """Re-arm level per channel for a hysteresis fraction frac_q8 / 256 (mkid_set_rearm): the level
+    moves from the threshold toward 0 (the baseline): lvl = thr - floor(thr * frac_q8 / 256).
+    frac_q8 = 0 gives lvl = thr (the round-1..4 rule)."""
+    t = np.asarray(thr, np.int64)
+    return (t - ((t * int(frac_q8)) >> 8)).astype(np.int32)
+
+
 class Trigger:
     """Streaming trigger over [J][C] int16 raw phase."""
 
     def __init__(self, C, taps, thr, mode=1, alpha=41, kf=82, kq=93623, base_thr=8192,
-                 dead=32):
+                 dead=32, rearm_q8=0):
         self.C = C
         self.taps = np.ascontiguousarray(taps, np.int16).reshape(C, 26)
         self.thr = np.ascontiguousarray(thr, np.int32).reshape(C)
+        self.rearm = np.ascontiguousarray(rearm_levels(self.thr, rearm_q8), np.int32)
         self.params = (mode, alpha, kf, kq, base_thr, dead)
         self.reset()
 
@@ -67,7 +76,7 @@ class Trigger:
         ev = np.zeros(max(cap, 1), np.uint64)
         counts = np.zeros(self.C, np.int64)
         mode, alpha, kf, kq, bt, dead = self.params
-        n = lib().oracle_trigger(_p(raw), J, self.C, _p(self.taps), _p(self.thr), mode, alpha, kf,
+        n = lib().oracle_trigger(_p(raw), J, self.C, _p(self.taps), _p(self.thr), _p(self.rearm), mode, alpha, kf,
                                  kq, bt, dead, _p(self.hist), _p(self.state), self.j0, _p(ev), cap,
                                  _p(counts))
         self.j0 += J

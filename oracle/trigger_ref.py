@@ -38,8 +38,10 @@ def new_state(C):
     return [dict(B=0, binit=0, st=DEAD, cnt=HOLDOFF, f1=0, f2=0, low=0, band=0) for _ in range(C)]
 
 
-def trigger(raw, taps, thr, mode, alpha, kf, kq, base_thr, dead, hist=None, state=None, j0=0):
-    """raw [J][C] int; taps [C][26]; returns (events list channel-major, hist, state)."""
+def trigger(raw, taps, thr, mode, alpha, kf, kq, base_thr, dead, hist=None, state=None, j0=0, rearm=None):
+    """raw [J][C] int; taps [C][26]; rearm [C] re-arm levels (None: the thresholds); returns
+    (events list channel-major, hist, state)."""
+    rearm = thr if rearm is None else rearm
     raw = np.asarray(raw, np.int64)
     J, C = raw.shape
     hist = np.zeros((25, C), np.int64) if hist is None else np.asarray(hist, np.int64).copy()
@@ -83,7 +85,7 @@ def trigger(raw, taps, thr, mode, alpha, kf, kq, base_thr, dead, hist=None, stat
                 if s['cnt'] <= 0:
                     s['st'] = REARM
             else:
-                if e >= thr[c]:
+                if e >= rearm[c]:
                     s['st'] = ARMED
             s['f2'] = s['f1']
             s['f1'] = f

@@ -34,7 +34,9 @@ def _witness_from_oracle(case, thr, mode, path, perturb=None):
     ev = trigger.Trigger(case.C, case.fir12, thr, mode=mode).run(r['raw'])[0]
     ph = r['phase'].astype(np.float32)
     if perturb == 'phase':
-        ph[5, 3] += 1e-4
+        ph[20, 3] += 1e-4     # a settled row (>= 16): the 1e-5 rad bar
+    if perturb == 'startup':
+        ph[3, 3] += 0.1       # row 3 (|y| = 0.006 |y|max, below the IQ floor): the absolute IQ bar
     if perturb == 'packet':
         ev = ev[1:]
     np.savez(path, phase=ph, raw=r['raw'], packets=ev)
@@ -66,7 +68,7 @@ def test_cpu_leg_witness_green(tmp_path, mode):
     assert ('%d packets' % npk) in out['one_core']['sample']
 
 
-@pytest.mark.parametrize('perturb', ['phase', 'packet'])
+@pytest.mark.parametrize('perturb', ['phase', 'startup', 'packet'])
 def test_cpu_leg_witness_red(tmp_path, perturb):
     case, thr, inp, cfgp = _case(tmp_path, 1)
     wit = str(tmp_path / 'wit.npz')
@@ -75,5 +77,9 @@ def test_cpu_leg_witness_red(tmp_path, perturb):
     assert p['green'] is False
     if perturb == 'packet':
         assert not p['packets_equal_on_device_raw'] and p['channels_diverged_without_flip'] == 1
+    elif perturb == 'phase':
+        assert p['phase_max_err_rad'] > 5e-5 and p['phase_max_err_settled_rad'] > 5e-5
     else:
-        assert p['phase_max_err_rad'] > 5e-5
+        assert p['phase_max_err_all_rows_rad'] > 5e-2 and p['phase_max_err_settled_rad'] < 1e-6
+        assert p['phase_max_err_rad'] < 1e-6 and p['samples_below_floor'] > 0
+        assert p['iq_err_below_floor_max_rel'] > 2e-7

@@ -57,8 +57,10 @@ def test_gpu_detector_against_truth(gpu):
         ch.set_dds(quiet.lut_i, quiet.lut_q)
         ch.set_lpf(quiet.lpf12)
         ch.set_fir(quiet.fir12)
+        ch.set_accumulator(True)
         ch.process(quiet.iq, want_phase=False)
         mi, mq = ch.avg_iq()
+        ch.set_accumulator(False)
         phi = np.arctan2(mq, mi)
         quiet = signals.make_case(C, S // 4, seed=seed, noise=noise, pulses_per_ch=0, dds_phase=phi)
         ch.set_dds(quiet.lut_i, quiet.lut_q)

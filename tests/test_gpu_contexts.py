@@ -140,7 +140,7 @@ def test_adc_and_phase_streams_do_not_mix(gpu):
 
 
 def test_timing_mask_and_counts_written_per_call(gpu):
-    """mkid_set_timing with MKID_TIMING_ONLY masks times only the named kernels (bench.py's timed
+    """mkid_set_timing_mask with MKID_TIMING_ONLY bits times only the named kernels (bench.py's timed
     steps record events around the front end alone); d_counts is written by each call's
     compaction (no zeroing launch), so stale values in it do not leak into the next call."""
     import torch
@@ -170,8 +170,17 @@ def test_timing_mask_and_counts_written_per_call(gpu):
             torch.cuda.synchronize()
             t = ch.timing()
             assert t['k_front'][1] == 1 and t['k_trigger'][1] == 1 and t['k_compact'][1] == 1
-            with pytest.raises(_lib.MkidError):   # bit 0 (every kernel) mixed with a mask
-                ch._chk(ch._L.mkid_set_timing(ch._h, 3))
+            with pytest.raises(_lib.MkidError):   # a bit past the last kernel
+                ch._chk(ch._L.mkid_set_timing_mask(ch._h, 1 << _lib.K_COUNT))
+            # mkid_set_timing keeps its round-1..3 meaning, any non-zero value times
+            # every kernel (the mask moved to its own entry point)
+            ch._chk(ch._L.mkid_set_timing(ch._h, -1))
+            ch._chk(ch._L.mkid_set_timing(ch._h, 2))
+            ch.process_device(x, S, None, ev, cap, cnt)
+            torch.cuda.synchronize()
+            t = ch.timing()
+            assert t['k_front'][1] == 1 and t['k_trigger'][1] == 1 and t['k_compact'][1] == 1
+            ch.set_timing(False)
             with pytest.raises(ValueError):
                 ch.set_timing(True, kernels=['no_such_kernel'])
             res.append((c, ev[:int(c[1])].cpu().numpy()))

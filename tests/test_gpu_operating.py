@@ -46,19 +46,16 @@ def _write_report(name, case, rep):
     if not d:
         return
     os.makedirs(d, exist_ok=True)
-    ymax = float(np.max(np.abs(case.loop_radius / case.loop_R)))
-    e, ymc = rep['err_rows'], rep['ymc']
-    settled = 16
+    e, ymc, ymax = rep['err_rows'], rep['ymc'], rep['ymax']
+    st = tp.SETTLE_ROWS
     with open(os.path.join(d, name + '.json'), 'w') as f:
-        json.dump({'C': case.C, 'rows': int(rep['rows']), 'amp': case.amps.tolist(),
-                   'loop_R': case.loop_R.tolist(), 'ymax': ymax,
-                   'radius_rel': (case.loop_radius / ymax).tolist(),
+        json.dump({'C': case.C, 'rows': int(rep['rows']), 'ymax': ymax, 'amp': case.amps.tolist(),
+                   'loop_R': case.loop_R.tolist(), 'radius_rel': (case.loop_radius / ymax).tolist(),
                    'err': np.asarray(rep['err']).tolist(), 'flips': np.asarray(rep['flips']).tolist(),
-                   'err_settled': e[settled:].max(axis=0).tolist(),
-                   'argmax_row': e.argmax(axis=0).tolist(),
-                   'ymc_min': ymc.min(axis=0).tolist(), 'ymc_min_settled': ymc[settled:].min(axis=0).tolist(),
+                   'err_settled': e[st:].max(axis=0).tolist(), 'argmax_row': e.argmax(axis=0).tolist(),
+                   'ymc_min': ymc.min(axis=0).tolist(), 'ymc_min_settled': ymc[st:].min(axis=0).tolist(),
                    'abs_iq_err': (e * ymc).max(axis=0).tolist(),
-                   'abs_iq_err_settled': (e[settled:] * ymc[settled:]).max(axis=0).tolist()}, f)
+                   'abs_iq_err_settled': (e[st:] * ymc[st:]).max(axis=0).tolist()}, f)
 
 
 @pytest.mark.parametrize('C,S,span,seed,splits', [

@@ -1,7 +1,10 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle on identical seeded inputs.
 
-Bars: phase within 1e-5 rad of the float64 oracle on every tone channel;
-Fix16_13 phase within 1 LSB (rounding-boundary flips only, rare); photon packets bit-exact —
+Bars: phase within 1e-5 rad of the float64 oracle on every tone channel at every
+sample where |y - c| >= the IQ floor F = IQ_TOL_REL / PHASE_TOL * |y|max (|y|max: the feedline's
+strongest tone); below it the phase of y - c is ill-conditioned in any precision (the stream's
+start-up, where y ramps from 0 through the loop centre; noise on a small loop), and the device is
+held to the absolute IQ bar |dphi| |y - c| <= IQ_TOL_REL |y|max instead; Fix16_13 phase within 1 LSB (rounding-boundary flips only, rare); photon packets bit-exact —
 both the full chain vs the oracle chain, and the device trigger vs the oracle trigger fed the
 device's own Fix16_13 phase.
 """
@@ -14,6 +17,14 @@ from oracle import trigger as otrig
 pytestmark = pytest.mark.gpu
 
 PHASE_TOL = 1e-5
+# absolute IQ error bar below the IQ floor, relative to the feedline's strongest tone |y| (the
+# comb's full-scale level). Measured (round 5): the device's y - c differs from the
+# float64 oracle's by <= 5e-8 |y|max on weak channels (the FFT's comb-level rounding), so the floor
+# F = 0.02 |y|max leaves a 4x margin.
+IQ_TOL_REL = 2e-7
+# rows after a reset until every tap of the chain sees stream samples: frame k is complete from
+# k = 2T - 1 = 7, output row j reads frames 2j + 1 - 25 .. 2j + 1, so j >= 16 (reporting only)
+SETTLE_ROWS = 16
 
 
 def configure(ch, case, thr, mode=1):
@@ -52,6 +63,7 @@ def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32, front='auto'):
     ch = Channelizer(case.C, max_chunk=max_chunk or S, dead_time=dead, front=front)
     try:
         configure(ch, case, thr, mode)
+        ch.set_accumulator(True)
         phases, evs = [], []
         for a, b in zip(splits[:-1], splits[1:]):
             ph, ev = ch.process(case.iq[a:b])
@@ -101,16 +113,21 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     err = np.abs(signals.wrap(ph_g[:, tones].astype(np.float64) - r['phase'][:, tones]))
     raw_g = np.clip(np.rint(ph_g * np.float32(8192)), -25736, 25736).astype(np.int64)
     draw = np.abs(raw_g[:, tones] - r['raw'][:, tones].astype(np.int64))
+    y_o = r['y'][:, tones]
+    ymc = np.abs(y_o - (case.ic[tones].astype(np.float64) + 1j * case.qc[tones].astype(np.float64)))
+    ymax = float(np.median(np.abs(y_o[SETTLE_ROWS:]), axis=0).max())
+    iq_tol = IQ_TOL_REL * ymax
     if report is not None:
-        report['err'] = err.max(axis=0)
-        report['flips'] = (draw > 0).sum(axis=0)
-        report['rows'] = err.shape[0]
-        report['err_rows'] = err
-        report['ymc'] = np.abs(r['y'][:, tones] - (case.ic[tones].astype(np.float64) +
-                                                   1j * case.qc[tones].astype(np.float64)))
-    tol = PHASE_TOL if phase_tol is None else np.asarray(phase_tol, np.float64)[tones]
-    bad = err.max(axis=0) >= tol
-    assert not bad.any(), 'phase error %.3g rad (%d channels over the bar)' % (err.max(), bad.sum())
+        report.update(err=err.max(axis=0), flips=(draw > 0).sum(axis=0), rows=err.shape[0], err_rows=err,
+                      ymc=ymc, ymax=ymax)
+    held = ymc >= iq_tol / PHASE_TOL                      # above the IQ floor
+    tol = PHASE_TOL if phase_tol is None else np.asarray(phase_tol, np.float64)[tones][None, :]
+    bad = held & (err >= tol)
+    assert not bad.any(), 'phase error %.3g rad (%d channels over the bar)' % (
+        err[held].max(), bad.any(axis=0).sum())
+    low = ~held & (err >= tol)                              # below it: the absolute IQ bar
+    assert not (low & (err * ymc > iq_tol)).any(), 'IQ error %.3g of |y|max below the floor' % (
+        (err * ymc)[low].max() / ymax)
 
     assert draw.max() <= 1
     assert (draw > 0).mean() < 5e-3
@@ -150,58 +167,19 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     (256, 2 ** 18, [0, 2 ** 16 + 512, 2 ** 17, 2 ** 18], 3, 'auto'),   # config 2, streamed
     (256, 2 ** 18, [0, 2 ** 16 + 512, 2 ** 17, 2 ** 18], 3, 'split'),
     (512, 2 ** 18, None, 4, 'auto'),
+    (512, 2 ** 19, [0, 2 ** 17 + 1024, 2 ** 19], 7, 'auto'),   # N = 1024 streamed (k_front3<1024>)
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'auto'),    # config 3 geometry
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'split'),
     (2048, 2 ** 20, [0, 3 * 2 ** 17 + 4096, 2 ** 20], 6, 'auto'),   # config 5 geometry (k_front5)
     (2048, 2 ** 20, None, 6, 'split'),
 ])
 def test_chain_parity(gpu, C, S, splits, seed, front):
-    """Full chain vs the oracle. 'auto' runs the fused front end (k_front3 for N = 512 and 2048,
-    k_front2 for N = 1024, k_front5 for N = 4096, k_front for N = 128); 'split' runs k_channelize +
-    k_lpf_phase with z staged in HBM."""
+    """Full chain vs the oracle. 'auto' runs the fused front end (k_front3 for N = 512 / 1024 / 2048,
+    k_front5 for N = 4096, k_front for N = 128); 'split' runs k_channelize + k_lpf_phase with z staged
+    in HBM. (Round 5 retired k_front2 and k_front4; their MKID_FRONT_V3=0 / MKID_FRONT_V5=0 cases
+    run through these default paths.)"""
     case, thr = cached_case(C, S, seed, max(1.0, S / (2 * C) / 400))
     compare(case, thr, splits or [0, S], front=front)
-
-
-def test_chain_parity_front2_at_2048(gpu, monkeypatch):
-    """The non-specialised k_front2 at N = 2048 (MKID_FRONT_V3=0; the default there is k_front3)
-    on config 3's parity case."""
-    monkeypatch.setenv('MKID_FRONT_V3', '0')
-    C, S = 1024, 2 ** 20
-    case, thr = cached_case(C, S, 5, max(1.0, S / (2 * C) / 400))
-    compare(case, thr, [0, 2 ** 19, S])
-
-
-def test_chain_parity_front2_at_512(gpu, monkeypatch):
-    """The non-specialised k_front2 at N = 512 (MKID_FRONT_V3=0; the default there is k_front3<512>
-    since round 4) on config 2's streamed parity case."""
-    monkeypatch.setenv('MKID_FRONT_V3', '0')
-    C, S = 256, 2 ** 18
-    case, thr = cached_case(C, S, 3, max(1.0, S / (2 * C) / 400))
-    compare(case, thr, [0, 2 ** 16 + 512, 2 ** 17, S])
-
-
-def test_chain_parity_front4_at_4096(gpu, monkeypatch):
-    """The non-specialised k_front4 at N = 4096 (MKID_FRONT_V5=0; the default there is the
-    wave-specialised k_front5) on config 5's parity case, streamed; and the two kernels' avgIQ
-    sums (the loop-calibration accumulator) agree to fp32 rounding."""
-    from mkids_sdr_amd.channelizer import Channelizer
-    monkeypatch.setenv('MKID_FRONT_V5', '0')
-    C, S = 2048, 2 ** 20
-    case, thr = cached_case(C, S, 6, max(1.0, S / (2 * C) / 400))
-    compare(case, thr, [0, 3 * 2 ** 17 + 4096, S])
-    sums = {}
-    for v in ('0', '1'):
-        monkeypatch.setenv('MKID_FRONT_V5', v)
-        ch = Channelizer(C, max_chunk=S)
-        try:
-            configure(ch, case, thr)
-            ch.process(case.iq)
-            sums[v] = np.asarray(ch.avg_iq())
-        finally:
-            ch.close()
-    scale = np.abs(sums['0']).max()
-    assert np.abs(sums['1'] - sums['0']).max() <= 1e-5 * scale
 
 
 @pytest.mark.parametrize('mode', [0, 1, 2])

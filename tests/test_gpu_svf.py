@@ -27,7 +27,7 @@ def synth_raw(C, J, seed, pulse_rate=1.0 / 2000):
     return np.clip(np.rint(ph), -25736, 25736).astype(np.int16)
 
 
-def run_both(raw, chunks, env=None, monkeypatch=None, max_events_per_ch=0):
+def run_both(raw, chunks, env=None, monkeypatch=None, max_events_per_ch=0, mode=2, rearm_q8=0):
     from mkids_sdr_amd.channelizer import Channelizer
     C = raw.shape[1]
     mf = codecs.fir_quantise(np.loadtxt(os.path.join(GOLD, 'fir', 'matched_30us.txt')))
@@ -40,7 +40,9 @@ def run_both(raw, chunks, env=None, monkeypatch=None, max_events_per_ch=0):
     try:
         ch.set_fir(taps)
         ch.set_thresholds(thr)
-        ch.set_baseline(2, 41, 82, 93623, 8192)
+        ch.set_baseline(mode, 41, 82, 93623, 8192)
+        if rearm_q8:
+            ch.set_rearm(rearm_q8)
         got, reruns, r0 = [], 0, 0
         for n in chunks:
             got.append(ch.trigger_phase(raw[r0:r0 + n]))
@@ -48,7 +50,7 @@ def run_both(raw, chunks, env=None, monkeypatch=None, max_events_per_ch=0):
             r0 += n
     finally:
         ch.close()
-    tr = otrig.Trigger(C, taps, thr, mode=2)
+    tr = otrig.Trigger(C, taps, thr, mode=mode, rearm_q8=rearm_q8)
     exp, r0 = [], 0
     for n in chunks:
         exp.append(tr.run(raw[r0:r0 + n])[0])
@@ -94,3 +96,71 @@ def test_svf_forced_fixup_small_event_cap(gpu, monkeypatch):
     for g, e in zip(got, exp):
         assert np.array_equal(g, e)
     assert reruns > 50
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('mode,rearm_q8,warmup', [
+    (2, 128, None),     # SVF, re-arm half way to the baseline
+    (2, 256, None),     # SVF, re-arm at the baseline
+    (2, 192, 520),      # SVF, forced fix-up re-runs (the speculative walk cannot settle)
+    (1, 160, None),     # EMA with hysteresis
+])
+def test_rearm_hysteresis_exact(gpu, monkeypatch, mode, rearm_q8, warmup):
+    """The re-arm level (mkid_set_rearm): the device's speculative segments +
+    exact fix-up against the sequential oracle with the same levels, bit for bit, streamed; and the
+    hysteresis removes packets (fewer than without it on the same rows)."""
+    C, J = 128, 160000
+    raw = synth_raw(C, J, 6 + rearm_q8)
+    env = {'MKID_SVF_WARMUP': warmup} if warmup else None
+    got, exp, reruns = run_both(raw, [70000, 90000], env=env, monkeypatch=monkeypatch, mode=mode,
+                                rearm_q8=rearm_q8)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    if warmup:
+        assert reruns > 50
+    _, exp0, _ = run_both(raw[:20000], [20000], mode=mode)
+    _, exp1, _ = run_both(raw[:20000], [20000], mode=mode, rearm_q8=rearm_q8)
+    assert len(exp1[0]) <= len(exp0[0])
+
+
+@pytest.mark.gpu
+def test_fused_ema_then_svf_switch(gpu):
+    """a fused-front-end context (k_front3, 1024 channels) runs EMA, is switched to SVF
+    by mkid_set_baseline mid-stream (the filter pre-pass rows are allocated then) and processes two
+    unequal calls; its packets equal the oracle trigger's on the device's own Fix16_13 phase, with
+    the same mode switch at the same row."""
+    import signals
+    from mkids_sdr_amd.channelizer import Channelizer
+    C = 1024
+    N = 2 * C
+    case = signals.make_case(C, 6 * 2 ** 18, seed=71, pulses_per_ch=3.0)
+    quiet = signals.make_case(C, 2 ** 20, seed=71, pulses_per_ch=0)
+    thr = signals.thresholds_from_quiet(quiet, signals.oracle_chain(quiet).process(quiet.iq)['raw'])
+    cuts = [0, 2 ** 19, 2 ** 19 + 3 * 2 ** 17 + N, 6 * 2 ** 18]
+    ch = Channelizer(C, max_chunk=2 ** 20)
+    try:
+        ch.set_pfb(case.pfb)
+        ch.set_bins(case.bins)
+        ch.set_dds(case.lut_i, case.lut_q)
+        ch.set_lpf(case.lpf12)
+        ch.set_fir(case.fir12)
+        ch.set_centers(case.ic, case.qc)
+        ch.set_thresholds(thr)
+        ch.set_baseline(1, 41, 82, 93623, 8192)
+        ph, ev = [], []
+        for i, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+            if i == 1:
+                ch.set_baseline(2, 41, 82, 93623, 8192)
+            p, e = ch.process(case.iq[a:b])
+            ph.append(p)
+            ev.append(e)
+    finally:
+        ch.close()
+    tr = otrig.Trigger(C, case.fir12, thr, mode=1)
+    for i, p in enumerate(ph):
+        if i == 1:
+            tr.params = (2,) + tr.params[1:]
+        raw = np.clip(np.rint(p * np.float32(8192)), -25736, 25736).astype(np.int16)
+        e_o = tr.run(raw)[0]
+        assert np.array_equal(np.sort(ev[i]), np.sort(e_o)), 'call %d' % i
+    assert sum(len(e) for e in ev[1:]) > 100

@@ -88,8 +88,10 @@ def test_packet_decode_roundtrip():
     assert out[7][0][3] == pytest.approx((p1 - 2048) * 360. / 2 ** 12 * 4 / np.pi)
 
 
-@pytest.mark.parametrize('mode', [0, 1, 2])
-def test_trigger_c_equals_python(oracle_lib, mode):
+@pytest.mark.parametrize('mode,rearm_q8', [(0, 0), (1, 0), (2, 0), (1, 128), (2, 200), (2, 256)])
+def test_trigger_c_equals_python(oracle_lib, mode, rearm_q8):
+    """The C trigger and its pure-Python twin, written independently, agree packet for packet;
+    rearm_q8 > 0 exercises the re-arm hysteresis (mkid_set_rearm levels)."""
     rng = np.random.default_rng(mode)
     C, J = 4, 2500
     raw = (rng.normal(0, 120, (J, C)) + 2000).astype(np.int64)
@@ -100,10 +102,11 @@ def test_trigger_c_equals_python(oracle_lib, mode):
     raw = np.clip(raw, -25736, 25736).astype(np.int16)
     taps = np.tile(setup_ref.fir_quantise(np.loadtxt(golden('fir/matched_30us.txt'))), (C, 1))
     thr = np.array([-1400, -2000, -900, -1500]) if mode else np.array([1000, 800, 1200, 900])
-    t = trigger.Trigger(C, taps, thr, mode=mode, dead=20)
+    t = trigger.Trigger(C, taps, thr, mode=mode, dead=20, rearm_q8=rearm_q8)
     e1, _, _ = t.run(raw[:1111])
     e2, _, _ = t.run(raw[1111:])
-    ev, _, _ = trigger_ref.trigger(raw, taps, thr, mode, 41, 82, 93623, 8192, 20)
+    lv = [int(v) - ((int(v) * rearm_q8) >> 8) for v in thr]     # floor division, restated
+    ev, _, _ = trigger_ref.trigger(raw, taps, thr, mode, 41, 82, 93623, 8192, 20, rearm=lv)
     key = lambda w: ((int(w) >> 52), int(w) & ((1 << 28) - 1))
     assert sorted(map(int, e1.tolist() + e2.tolist()), key=key) == sorted(map(int, ev), key=key)
     assert len(ev) >= 10

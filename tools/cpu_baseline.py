@@ -57,7 +57,8 @@ def _trigger(trigger, cfg):
     """The oracle trigger in the bench step's baseline mode (EMA 1 / SVF 2, register constants
     of set_alpha.py / set_svf.py / set_base_thresh.py)."""
     mode = int(cfg['mode']) if 'mode' in cfg else 1
-    return trigger.Trigger(int(cfg['C']), cfg['fir'], cfg['thr'], mode=mode)
+    q8 = int(cfg['rearm_q8']) if 'rearm_q8' in cfg else 0
+    return trigger.Trigger(int(cfg['C']), cfg['fir'], cfg['thr'], mode=mode, rearm_q8=q8)
 
 
 def run_chunk(args, collect=None):
@@ -91,6 +92,9 @@ def run_chunk(args, collect=None):
         ev, k, _ = tr.run(r['raw'])
         nev += k
         if collect is not None:
+            cen = o.ic[None, :] + 1j * o.qc[None, :]
+            collect.setdefault('ymc', []).append(np.abs(r['y'] - cen).astype(np.float32))
+            collect.setdefault('ymed', []).append(np.median(np.abs(r['y']), axis=0))
             collect.setdefault('phase', []).append(r['phase'])
             collect.setdefault('raw', []).append(r['raw'])
             collect.setdefault('packets', []).append(ev)
@@ -139,6 +143,14 @@ def witness_compare(col, witp, cfg):
     C = int(cfg['C'])
     assert dph.shape == oph.shape == draw.shape, (dph.shape, oph.shape, draw.shape)
     err = np.abs((dph.astype(np.float64) - oph + np.pi) % (2 * np.pi) - np.pi)
+    # the bars of tests/test_gpu_parity.py: 1e-5 rad at every sample above the IQ floor
+    # |y - c| >= 0.02 |y|max; below it the absolute IQ bar |dphi| |y - c| <= 2e-7 |y|max
+    ymc = np.concatenate(col['ymc']).astype(np.float64)
+    settle = 16
+    ymax = float(np.max(np.median(np.stack(col['ymed']), axis=0)))   # |y|max: the strongest tone
+    held = ymc >= 0.02 * ymax
+    low = ~held & (err >= 1e-5)
+    iq_rel = float((err * ymc)[low].max() / ymax) if low.any() and ymax > 0 else 0.0
     dr = draw.astype(np.int32) - oraw.astype(np.int32)
     flips = dr != 0
     own = _trigger(trigger, cfg).run(draw)[0]
@@ -154,8 +166,12 @@ def witness_compare(col, witp, cfg):
     flip_ch = set(np.nonzero(flips.any(axis=0))[0].tolist())
     unexplained = [c for c in diverged if c not in flip_ch]
     out = dict(samples=int(dph.shape[0] * 2 * C), rows=int(dph.shape[0]), channels=C,
-               phase_max_err_rad=float(err.max()), phase_p999999_err_rad=float(np.quantile(err, 0.999999)),
-               phase_tol_rad=1e-5,
+               phase_max_err_rad=float(err[held].max()),
+               phase_max_err_all_rows_rad=float(err.max()),
+               phase_max_err_settled_rad=float(err[settle:].max()) if err.shape[0] > settle else None,
+               phase_p999999_err_rad=float(np.quantile(err, 0.999999)),
+               phase_tol_rad=1e-5, iq_err_below_floor_max_rel=iq_rel, iq_tol_rel=2e-7,
+               iq_floor_rel=0.02, samples_below_floor=int((~held).sum()), settle_rows=settle,
                raw_flip_rate=float(flips.mean()), raw_max_abs_diff=int(np.abs(dr).max()),
                channels_with_flip=len(flip_ch),
                packets_device=int(dpk.size), packets_oracle_chain=int(opk.size),
@@ -178,8 +194,8 @@ def witness_compare(col, witp, cfg):
                                 for lo, hi in ((0.0, 0.3), (0.3, 1.0), (1.0, 10.0), (10.0, np.inf))
                                 for m in [(ratio >= lo) & (ratio < hi) if np.isfinite(hi) else ratio >= lo]]
         out['by_loop_ratio'][-1]['ratio'] = [10.0, 'inf (centre at the origin)']
-    green = (out['phase_max_err_rad'] <= 1e-5 and out['raw_max_abs_diff'] <= 1 and own_equal
-             and not unexplained)
+    green = (out['phase_max_err_rad'] <= 1e-5 and iq_rel <= 2e-7 and out['raw_max_abs_diff'] <= 1
+             and own_equal and not unexplained)
     if 'heights' in w.files:
         sys.path.insert(0, ROOT)
         from oracle import heights as oh

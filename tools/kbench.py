@@ -88,9 +88,13 @@ def main():
             ch.synth_adc(x, S, 0, base, d_tones, d_pul, len(ps), 0.1 * N, 65.0 * N, 390 * N, sigma, 42)
             ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
             ch.set_thresholds(np.full(C, -(1 << 30), np.int32))
+            if hasattr(ch._L, 'mkid_set_accumulator'):   # older variants accumulate on every call
+                ch.set_accumulator(True)
             ch.process_device(x, S, phase, d_ev, cap, d_cnt)
             torch.cuda.synchronize()
             mi, mq = ch.avg_iq()
+            if hasattr(ch._L, 'mkid_set_accumulator'):
+                ch.set_accumulator(False)
             cal = np.arctan2(mq, mi)
         dds = lut.define_dds_lut(list(np.asarray(feed['f_rf'])[perm]), feed['f_base'], C, fs, phase=cal[perm])
         assert np.array_equal(np.asarray(dds['bins']) % N, np.asarray(feed['dds']['bins'])[perm] % N)

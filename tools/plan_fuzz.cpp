@@ -21,7 +21,8 @@ typedef struct {
     int64_t low, band;
 } trig_state;
 void oracle_trig_reset_state(trig_state* st, int32_t C);
-int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* taps, const int32_t* thr, int32_t mode,
+int64_t oracle_trigger(const int16_t* raw, int64_t J, int32_t C, const int16_t* taps, const int32_t* thr,
+                       const int32_t* rearm, int32_t mode,
                        int32_t alpha, int32_t kf, int32_t kq, int32_t base_thr, int32_t dead, int16_t* hist,
                        trig_state* st, int64_t j0, uint64_t* ev, int64_t cap, int64_t* counts);
 }
@@ -138,10 +139,12 @@ static void fuzz_capacity(int iters) {
         const int dead = (int)rint_(0, 40);
         const int mode = (int)rint_(0, 2);
         std::vector<int16_t> raw((size_t)(J * C)), taps((size_t)C * 26, 0), hist((size_t)25 * C, 0);
-        std::vector<int32_t> thr(C);
+        std::vector<int32_t> thr(C), rearm(C);
+        const int64_t q8 = rint_(0, 256);         // re-arm hysteresis (mkid_set_rearm)
         for (int c = 0; c < C; ++c) {
             taps[(size_t)c * 26] = 2047;          // identity matched filter: f = raw * 2047 >> 11
             thr[c] = (int32_t)rint_(-3000, 3000);
+            rearm[c] = rearm_level(thr[c], (int32_t)q8);
         }
         const int kind = (int)rint_(0, 2);
         for (int64_t j = 0; j < J; ++j)
@@ -157,7 +160,7 @@ static void fuzz_capacity(int iters) {
         const int64_t cap = J * C;
         std::vector<uint64_t> ev((size_t)cap);
         std::vector<int64_t> counts(C);
-        const int64_t total = oracle_trigger(raw.data(), J, C, taps.data(), thr.data(), mode, 41, 82, 93623,
+        const int64_t total = oracle_trigger(raw.data(), J, C, taps.data(), thr.data(), rearm.data(), mode, 41, 82, 93623,
                                              mode ? 8192 : 0, dead, hist.data(), st.data(), 0, ev.data(), cap,
                                              counts.data());
         CHECK(total <= cap, "trigger overflowed its own bound");

@@ -9,6 +9,11 @@ before it (bench.py's window: -2 .. +60 rows); the unmatched ones are histogramm
 after that pulse and by the pulse's amplitude, and the baseline e = f - B at the packet is kept.
 
     python tools/svf_characterize.py [--rows 400000] [--channels 64] > profiles/r03_svf_unmatched.json
+    python tools/svf_characterize.py --rearm 0,64,128,192,256   # re-arm hysteresis (mkid_set_rearm)
+
+Round 5 adds the re-arm level (hysteresis, mkid_set_rearm): each (mode, rearm_q8) pair reports the
+unmatched packets per pulse and the pulses that got no packet at all (missed), so the price of the
+later re-arm (a pulse on the previous pulse's tail) is measured beside its benefit.
 """
 import argparse
 import json
@@ -40,6 +45,7 @@ def main():
     ap.add_argument('--rows', type=int, default=400000)
     ap.add_argument('--channels', type=int, default=64)
     ap.add_argument('--rate', type=float, default=1.0 / 2048)
+    ap.add_argument('--rearm', default='0', help='comma-separated re-arm fractions (/256) to evaluate')
     a = ap.parse_args()
     from oracle import trigger
     from mkids_sdr_amd import codecs
@@ -53,14 +59,17 @@ def main():
     for s0, c, amp in pulses:
         byc.setdefault(c, []).append((s0, amp))
     out = dict(rows=J, channels=C, pulses=len(pulses), sigma_raw=300, thresholds_median=int(np.median(thr)))
-    for name, mode in (('ema', 1), ('svf', 2)):
-        ev = trigger.Trigger(C, taps, thr, mode=mode).run(raw)[0]
+    runs = [(('ema' if mode == 1 else 'svf') + ('' if q == 0 else '_rearm%d' % q), mode, q)
+            for q in [int(v) for v in a.rearm.split(',')] for mode in (1, 2)]
+    for name, mode, q8 in runs:
+        ev = trigger.Trigger(C, taps, thr, mode=mode, rearm_q8=q8).run(raw)[0]
         u = codecs.unpack_wide(ev)
         ch = np.asarray(u['ch'] if isinstance(u, dict) else u[0])
         ts = np.asarray(u['ts'] if isinstance(u, dict) else u[3]).astype(np.int64)
         base = np.asarray(u['base'] if isinstance(u, dict) else u[2])
         delays, amps, unmatched, matched = [], [], 0, 0
         nop = 0
+        hit = set()
         for c_, t_ in zip(ch.tolist(), ts.tolist()):
             ps = byc.get(c_, [])
             starts = np.array([p[0] for p in ps]) if ps else np.zeros(0, np.int64)
@@ -72,14 +81,18 @@ def main():
             d = t_ - int(starts[k])
             if -2 <= d <= 60:
                 matched += 1
+                hit.add((c_, int(starts[k])))
             else:
                 unmatched += 1
                 delays.append(d)
                 amps.append(ps[k][1])
         delays = np.asarray(delays)
         amps = np.asarray(amps)
-        rec = dict(packets=int(len(ev)), matched=matched, unmatched=unmatched, unmatched_before_any_pulse=nop,
-                   unmatched_per_pulse=round(unmatched / max(1, len(pulses)), 4))
+        rec = dict(rearm_q8=q8, packets=int(len(ev)), matched=matched, unmatched=unmatched,
+                   unmatched_before_any_pulse=nop,
+                   unmatched_per_pulse=round(unmatched / max(1, len(pulses)), 4),
+                   pulses_missed=int(len(pulses) - len(hit)),
+                   missed_per_pulse=round((len(pulses) - len(hit)) / max(1, len(pulses)), 4))
         if len(delays):
             edges = [61, 100, 150, 200, 300, 400, 600, 1000, 2000, 10 ** 9]
             h = np.histogram(delays, bins=edges)[0]

@@ -59,7 +59,7 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=10)
     # the first launches of a fresh process run slower while the clock ramps (rocprofv3 traces,
-    # profiles/r04_v_*: config 3 k_front3 4.99, 4.65, 4.33, 4.30 ms then ~4.25; config 5 6.69 ->
+    # profiles/r04/r04_v_*: config 3 k_front3 4.99, 4.65, 4.33, 4.30 ms then ~4.25; config 5 6.69 ->
     # 5.45 over six launches): ten untimed steps reach the steady state of a continuous stream
     p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--config', type=int, default=3, choices=sorted(CONFIGS))
@@ -479,7 +479,7 @@ def main():
 
     # per-kernel breakdown (kernel_ms) from the last warm-up steps, every kernel timed; the timed
     # steps below time only the front end (the roofline kernel): each timed launch records two
-    # HIP events, and an event record costs ~5 us of stream time (profiles/r04_v traces), ~2 % of
+    # HIP events, and an event record costs ~5 us of stream time (profiles/r04/r04_v traces), ~2 % of
     # a config-2 step if every kernel were timed
     nbreak = min(3, args.warmup)
     for i in range(args.warmup):

@@ -57,7 +57,7 @@
 // once, so neither should evict the LO table (512 KB at 1024 channels, re-read by every
 // workgroup every iteration) from L2. With default-policy streams the LO rows miss L2 on some
 // boxes and their loads stall the select stage: same-box A/B -15 % k_front, -11 % k_trigger
-// (profiles/r01_v29_kbench_nt.json). 0 restores default-policy accesses for A/B.
+// (profiles/r01/r01_v29_kbench_nt.json). 0 restores default-policy accesses for A/B.
 
 namespace mkid {
 
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
     // static issue priority by dispatch order (MI355X_MICROARCH.md "two waves per SIMD" item 4):
     // the later-dispatched waves of a SIMD lose every age-based arbitration and reach each barrier
     // last; raising them once before the loop trims that skew (-0.7..-1 % k_front, same-box A/B
-    // profiles/r01_v28_kbench_prio.json)
+    // profiles/r01/r01_v28_kbench_prio.json)
     {
         const int w = __builtin_amdgcn_readfirstlane(tid) / 64, nw = G::BT / 64;
         const int pr = nw >= 4 ? w * 4 / nw : 0;  // 0..3 by quarter of the workgroup

@@ -1,5 +1,5 @@
 // Fused front end k_front3 (the default at N = 2048, config 3/4, and since round 4 at N = 512,
-// config 2: -5.3 % same-box, profiles/r04_k_kbench_f3_512_vs_f2.json): k_front2's arithmetic
+// config 2: -5.3 % same-box, profiles/r04/r04_k_kbench_f3_512_vs_f2.json): k_front2's arithmetic
 // (k_front2.hip) with wave specialisation.
 #include "front_common.h"
 

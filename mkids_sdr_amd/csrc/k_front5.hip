@@ -60,7 +60,9 @@ struct G5 {
     static constexpr int FB = NW * REG;           // float2 per frame
     static constexpr int HIST = (2 * T - 1 + kLpfHist) * M;
     static constexpr size_t off_fbuf = (size_t)RS * M * 4;
-    static constexpr size_t off_ysum = off_fbuf + (size_t)2 * FB * 8;  // [C] float2 avgIQ partial sums
+    // [C] float2 per-channel slot: the avgIQ partial sums while the accumulator is armed
+    // (k_front5<true>), else the centring constant -c' (k_front5<false>, the streaming kernel)
+    static constexpr size_t off_ysum = off_fbuf + (size_t)2 * FB * 8;
     static constexpr size_t lds_bytes = off_ysum + (size_t)C * 8;
     static_assert(SPT == 8 && SPW * FW == NW, "geometry");
     static_assert(SW3 * 64 * 3 + (SW - SW3) * 64 * 2 == C, "every channel has one select slot");
@@ -100,10 +102,11 @@ __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 
 // measured and dropped (DESIGN.md §5 k_front5): T1 in registers, LO one frame ahead, one Horner
 // chain, even/odd chains, unsplit Y reads, no barrier between channels, transform-wave priority
 
-// select / DDC / low-pass / phase of CPT channels c0 + cs q per thread, frame k - 1 of iteration t
-// (the centring constants -c' and r, mkid_internal.h Centring, are re-read from global memory with
-// the frame's LO row and the avgIQ sums kept in LDS ysl: registers go to the low-pass state)
-template <int CPT>
+// select / DDC / low-pass / phase of CPT channels c0 + cs q per thread, frame k - 1 of iteration t.
+// Registers go to the low-pass state: the centring constants (mkid_internal.h Centring) are re-read
+// per frame, -c' from the per-channel LDS slot ysl (ACC = false) or, while the avgIQ accumulator
+// is armed and ysl holds its partial sums (ACC = true), from global memory; r at output frames.
+template <int CPT, bool ACC>
 __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0, int cs,
                                            int64_t k_b, int64_t k_start, int nrun, int nit) {
     constexpr int C = G5::C;
@@ -117,7 +120,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
         sincospi(-2.0 * (double)bin / G5::N, &sn, &cn);
         tb[q] = make_float2((float)cn, (float)sn);
         yoff[q] = yswz(bin & 511);
-        if (a.ysum) ysl[c] = make_float2(0.f, 0.f);
+        ysl[c] = ACC ? make_float2(0.f, 0.f) : a.cen.ncen[c];   // the thread's own channels only
     }
     uint64_t gp[13];
 #pragma unroll
@@ -158,7 +161,8 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
 #pragma unroll
                 for (int q = 0; q < CPT; ++q) {
                     lov[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
-                    ncv[q] = *reinterpret_cast<const float2*>(ncrow + (uint32_t)(cb + cs * q) * 8u);
+                    ncv[q] = ACC ? *reinterpret_cast<const float2*>(ncrow + (uint32_t)(cb + cs * q) * 8u)
+                                 : ysl[cb + cs * q];
                 }
             }
             [[maybe_unused]] float2 corv[CPT];
@@ -216,7 +220,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                         // reference accumulates on demand, startAccumulator / avgIQ_ctrl,
                         // ROACH_Setup.py:654-659). One owner per entry: a plain read-add-write (LDS
                         // float atomics stalled every wave's LDS traffic on output frames)
-                        if (a.ysum) {
+                        if (ACC) {
                             float2 ysv = ysl[c];
                             ysv.x += y.x;
                             ysv.y += y.y;
@@ -257,7 +261,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
     };
     for (int p = 0; p < kLpfHist / 2; ++p) pair(p, std::false_type{});
     for (int p = kLpfHist / 2; p < nit / 2; ++p) pair(p, std::true_type{});
-    if (a.ysum)
+    if (ACC)
 #pragma unroll
         for (int q = 0; q < CPT; ++q) {
             const float2 ys = ysl[c0 + cs * q];
@@ -267,6 +271,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
 
 }  // namespace
 
+template <bool ACC>
 __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
     using G = G5;
     constexpr int NW = G::NW, M = G::M, T = G::T, RS = G::RS;
@@ -404,15 +409,16 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
         // ---------------- select waves, one frame behind the transform waves --------------------
         const int sw = wave - G::FW;
         if (sw < G::SW3)
-            select_run<3>(a, fbuf, ysl, sw * 64 + L, 512, k_b, k_start, nrun, nit);
+            select_run<3, ACC>(a, fbuf, ysl, sw * 64 + L, 512, k_b, k_start, nrun, nit);
         else
-            select_run<2>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64 + L, 256, k_b, k_start, nrun, nit);
+            select_run<2, ACC>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64 + L, 256, k_b, k_start, nrun, nit);
     }
 }
 
 hipError_t launch_front5(const FrontArgs& a0, hipStream_t s) {
-    static std::atomic<uint64_t> attr_mask{0};
-    hipError_t e = ensure_lds_attr(attr_mask, (const void*)k_front5, (int)G5::lds_bytes);
+    static std::atomic<uint64_t> attr_mask{0}, attr_mask_acc{0};
+    const void* fn = a0.ysum ? (const void*)k_front5<true> : (const void*)k_front5<false>;
+    hipError_t e = ensure_lds_attr(a0.ysum ? attr_mask_acc : attr_mask, fn, (int)G5::lds_bytes);
     if (e != hipSuccess) return e;
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
@@ -424,7 +430,10 @@ hipError_t launch_front5(const FrontArgs& a0, hipStream_t s) {
     fpb = (fpb + 1) / 2 * 2;
     a.frames_per_block = fpb;
     const int64_t blocks = (a.K + fpb - 1) / fpb;
-    hipLaunchKernelGGL(k_front5, dim3((unsigned)blocks), dim3(G5::BT), G5::lds_bytes, s, a);
+    if (a.ysum)
+        hipLaunchKernelGGL(k_front5<true>, dim3((unsigned)blocks), dim3(G5::BT), G5::lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL(k_front5<false>, dim3((unsigned)blocks), dim3(G5::BT), G5::lds_bytes, s, a);
     return hipGetLastError();
 }
 

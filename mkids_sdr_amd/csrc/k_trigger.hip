@@ -124,7 +124,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const char* base) {
 // Software pipeline over half groups of 13 samples: the loads of the next half are in flight
 // while the current half is processed (26 load registers, as for a whole-group batch, but no
 // wave waits a full memory latency per group). A whole group in flight ahead (52 registers, 2 waves
-// per SIMD) is +16 % at config 3 and flat at config 2 (profiles/r04_l_kbench_trig_deep_c*.json).
+// per SIMD) is +16 % at config 3 and flat at config 2 (profiles/r04/r04_l_kbench_trig_deep_c*.json).
 // body(group, u, raw) sees u = 0..25 in order and half_end(group, h) runs after each half group
 // (h = 0, 1); rrow advances by ngroups rows of 26. The last prefetch re-reads the current group.
 template <class F, class E>
@@ -214,14 +214,14 @@ struct Stepper<MKID_BASE_SVF, true> {
 
 // 4 waves per SIMD (128 VGPRs; the occupancy also sizes the segments, mkid_plan.cpp): -4.4 %
 // k_trig_spec at 1024 channels and -5.4 % at 2048 against 3 waves (135 VGPRs), neutral at 256
-// (profiles/r04_ag_kbench_*.json); the few spilled dwords are outside the sample loops
+// (profiles/r04/r04_ag_kbench_*.json); the few spilled dwords are outside the sample loops
 #ifndef MKID_TRIG_MINW
 #define MKID_TRIG_MINW 4
 #endif
 // Issue priority falls with the wave's progress through its segment (done of ng groups): the
 // SIMD's older waves otherwise win every arbitration, finish first and leave the youngest to run
 // alone at a lone wave's issue rate. Priority 3 -> 2 -> 1 -> 0 at 70 / 85 / 95 % is -9 % k_trig_spec
-// at 1024 and 2048 channels, neutral at 256 (profiles/r04_p_*, r04_q_*).
+// at 1024 and 2048 channels, neutral at 256 (profiles/r04/r04_p_*, r04_q_*).
 __device__ __forceinline__ void set_progress_prio(int32_t done, int32_t ng) {
     const int32_t pc = done * 100;
     if (pc >= 95 * ng) __builtin_amdgcn_s_setprio(0);

@@ -83,6 +83,9 @@ struct mkid_ctx {
     hipEvent_t ev_start = nullptr, ev_done = nullptr;
     int zi = 0;
     int64_t G = 0;  // pipeline sub-chunk (samples)
+    // test hook (MKID_FAULT_LAUNCH=n at mkid_create): the n-th front-end launch of the context
+    // reports a HIP failure after it was enqueued, to test the state a partly enqueued call leaves
+    int64_t fault_launch = 0, launch_count = 0;
     int64_t last_raw_row = 0;       // first row of the last sub-chunk's raw phase in d_raw
     bool fused = false;  // K1-K6 in one kernel (k_front / k_front3 / k_front5: no z buffers, no stream B work)
     int64_t H = 0;       // ADC history samples carried between calls
@@ -301,6 +304,7 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     {
         const char* so = getenv("MKID_SLOT_ORDER");
         c->slot_order_on = !(so && atoi(so) == 0);
+        if (const char* fl = getenv("MKID_FAULT_LAUNCH")) c->fault_launch = atoll(fl);
     }
     int64_t trig_slots = trigger_wave_slots(device);
     // tuning/test knob: pretend the GPU holds this many trigger waves (forces longer segments)
@@ -716,7 +720,7 @@ static int compact_call(mkid_ctx* c, int32_t stride, int32_t capseg, uint64_t* d
 // compaction per call, all on the context stream. (Round 2 also had an opt-in two-stream pipeline
 // running a register-lean trigger beside the front end; it never paid — the front ends keep their
 // SIMDs ~77 % VALU-busy, and the lean kernel alone is no faster than k_trig_spec — and was removed
-// in round 3: profiles/r02_v7_kbench_pipeline.json, r03_h_kbench_trig_lean_standalone*.json.)
+// in round 3: profiles/r02/r02_v7_kbench_pipeline.json, r03_h_kbench_trig_lean_standalone*.json.)
 static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_phase, uint64_t* d_events,
                          int64_t cap, int64_t* d_counts) {
     const int C = c->C, N = c->N, M = c->M;
@@ -728,6 +732,9 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         int r = plan_call(c, n, subs, stride, capseg);
         if (r) return r;
     }
+    // planned: from the first launch on the context carries an ADC stream, even if a later step of
+    // this call fails (a failed planning / argument check leaves the stream kind as it was)
+    c->stream_kind = 1;
     const uint32_t* x = (const uint32_t*)d_iq;
     c->last_J = 0;
     int32_t seg_off = 0;
@@ -761,6 +768,8 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         tstart(c, MKID_K_FRONT, &kt, A);
         HIPCHK(c, launch_fused(N, fa, A));
         tstop(c, &kt, A);
+        if (c->fault_launch > 0 && ++c->launch_count == c->fault_launch)
+            FAIL(c, MKID_E_HIP, "injected launch failure (MKID_FAULT_LAUNCH)");
         const bool last = off + S >= n;
         int r = run_trigger(c, raw, subs[si], stride, seg_off, capseg, A, !last);
         if (r) return r;
@@ -798,6 +807,7 @@ static int process_split(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         int r = plan_call(c, n, subs, stride, capseg);
         if (r) return r;
     }
+    c->stream_kind = 1;   // planned (as process_fused)
     // B joins A's order (inputs written by earlier work on A, previous calls) ...
     HIPCHK(c, hipEventRecord(c->ev_start, A));
     HIPCHK(c, hipStreamWaitEvent(B, c->ev_start, 0));
@@ -881,9 +891,6 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     const int r = c->fused ? process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts)
                            : process_split(c, d_iq, n, d_phase, d_events, cap, d_counts);
     if (r == MKID_OK) acc_account(c, n / c->N);
-    // the context carries an ADC stream only once a call has been enqueued (a call that failed
-    // before, e.g. in planning, leaves the stream kind as it was)
-    if (r == MKID_OK) c->stream_kind = 1;
     return r;
 }
 
@@ -902,6 +909,7 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
         int r = plan_call(c, rows * c->N, subs, stride, capseg);
         if (r) return r;
     }
+    c->stream_kind = 2;   // planned: the context now carries a phase-row stream (as process_fused)
     int32_t seg_off = 0;
     int64_t r0 = 0;
     for (const SubPlan& sp : subs) {
@@ -911,9 +919,7 @@ int mkid_trigger_phase(mkid_ctx* c, const int16_t* d_raw, int64_t rows, uint64_t
         r0 += sp.J;
         c->j0 += sp.J;
     }
-    const int r = compact_call(c, stride, capseg, d_events, cap, d_counts, s);
-    if (r == MKID_OK) c->stream_kind = 2;   // as mkid_process_device: only once enqueued
-    return r;
+    return compact_call(c, stride, capseg, d_events, cap, d_counts, s);
 }
 
 int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, uint64_t* events_out, int64_t cap,

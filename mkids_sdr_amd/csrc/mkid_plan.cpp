@@ -119,7 +119,7 @@ const char* plan_call(const Workspace& ws, int C, int N, int mode, int dead, int
 // group whose cost rises least, then whose new cost is lowest, then the emptiest: ~1.9 cycles per
 // group (tools/lds_assign.py holds the same algorithm and its model).
 // k_front4 (C = 2048) has the same read pattern but loses with the order (+0.5 % with plain stores,
-// +2.6 % with its non-temporal ones: profiles/r03_h_kbench_f4_slot_order.json), so only k_front3
+// +2.6 % with its non-temporal ones: profiles/r03/r03_h_kbench_f4_slot_order.json), so only k_front3
 // takes it; mkid_slot_order still reports the C = 2048 order for the model and tests.
 void slot_order(const std::vector<int32_t>& bins, int C, std::vector<int16_t>& out) {
     out.resize(C);

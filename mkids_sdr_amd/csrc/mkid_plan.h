@@ -21,10 +21,10 @@ constexpr int kPfbTaps = 4;
 // The EMA baseline (alpha 41/512) forgets its start in ~10^2 samples on noisy phase. The warm-up is
 // pure overhead when the speculation holds and the fix-up re-runs a segment when it does not
 // (exact either way): on the bench stream 520 -> 260 samples is -6 % trigger time with no re-run,
-// 130 re-runs 427 segments per step and gains nothing (profiles/r04_j_kbench_trig_warmup.json).
+// 130 re-runs 427 segments per step and gains nothing (profiles/r04/r04_j_kbench_trig_warmup.json).
 // The floor kSegL only binds when the channels are few (256 at config 2: 2^28 samples give 2048
 // rows per channel-segment at one wave per SIMD); 2048 -> 1024 is -41 % k_trig_spec there, 512
-// no better, and config 3 / 5 segments are longer anyway (profiles/r04_o_kbench_c2.json).
+// no better, and config 3 / 5 segments are longer anyway (profiles/r04/r04_o_kbench_c2.json).
 constexpr int64_t kSegL = 1024;
 constexpr int64_t kSegW = 260;
 // SVF baseline (Chamberlin 2-pole, Kf 82 / Kq 93623 Fix18_16): two integer trajectories started

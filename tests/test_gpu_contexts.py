@@ -139,6 +139,37 @@ def test_adc_and_phase_streams_do_not_mix(gpu):
         ch.close()
 
 
+def test_failed_call_after_planning_marks_the_stream(gpu, monkeypatch):
+    """a process call that fails after its first launch was enqueued (here an injected
+    failure, MKID_FAULT_LAUNCH=1) has advanced the context's stream, so the context is marked as
+    carrying an ADC stream: a following mkid_trigger_phase fails with MKID_E_STATE. A call refused in
+    planning (a bad size) leaves the stream kind unchanged."""
+    from mkids_sdr_amd import _lib
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 64, 1 << 14
+    case = signals.make_case(C, S, seed=45, pulses_per_ch=0.0)
+    monkeypatch.setenv('MKID_FAULT_LAUNCH', '1')
+    ch = Channelizer(C, max_chunk=S)
+    monkeypatch.delenv('MKID_FAULT_LAUNCH')
+    try:
+        configure(ch, case, np.full(C, -(1 << 30)))
+        with pytest.raises(_lib.MkidError) as e:
+            ch.process(case.iq[:100])              # not a multiple of N: refused before planning
+        assert e.value.code == _lib.MKID_E_ARG
+        ch.trigger_phase(np.zeros((8, C), np.int16))   # still a fresh context: allowed
+        ch.reset()
+        with pytest.raises(_lib.MkidError) as e:
+            ch.process(case.iq)                    # the injected failure after the first launch
+        assert e.value.code == _lib.MKID_E_HIP and 'injected' in str(e.value)
+        with pytest.raises(_lib.MkidError) as e:
+            ch.trigger_phase(np.zeros((8, C), np.int16))
+        assert e.value.code == _lib.MKID_E_STATE
+        ch.reset()
+        ch.process(case.iq)                        # the hook fires once
+    finally:
+        ch.close()
+
+
 def test_timing_mask_and_counts_written_per_call(gpu):
     """mkid_set_timing_mask with MKID_TIMING_ONLY bits times only the named kernels (bench.py's timed
     steps record events around the front end alone); d_counts is written by each call's

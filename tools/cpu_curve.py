@@ -4,7 +4,7 @@ tools/cpu_baseline.py at several worker counts on a bench-like config-3 input ge
 (signals.make_case: 1024 ch, seeded tones + noise + pulses), to show where the box's CPU share
 saturates (the cgroup quota, not sched_getaffinity).
 
-    python tools/cpu_curve.py [--samples-log2 26] [--workers 4,8,16,32,64,256] > profiles/r03_cpu_curve.json
+    python tools/cpu_curve.py [--samples-log2 26] [--workers 4,8,16,32,64,256] > profiles/r03/r03_cpu_curve.json
 """
 import argparse
 import json

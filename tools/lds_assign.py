@@ -7,7 +7,7 @@ each into the group whose cost rises least, then the one it leaves lowest, then 
 `python tools/lds_assign.py` prints the modelled cost; tools/kbench.py's `lib.so#a` / `lib.so#b`
 relabel the bench feedline in these orders (the same physical tones, channels renumbered), which
 times the gather at the reduced conflict level with the kernel unchanged (round-3 A/B:
-profiles/r03_h_kbench_f3_slot_order.json)."""
+profiles/r03/r03_h_kbench_f3_slot_order.json)."""
 import numpy as np
 
 

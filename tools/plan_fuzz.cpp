@@ -130,6 +130,46 @@ static void fuzz_plans(int iters) {
     }
 }
 
+// Sizing-only pass at the bench's scale: max_chunk up to 2^31 samples and the trigger
+// slot / SVF lane counts of an MI355X (256 CUs; k_trig_spec at 4 blocks of 4 waves per CU; one SVF
+// segment per two SIMD lanes), so SVF segments longer than the EMA segment the slot table was sized
+// from are planned too. Every legal call (n <= max_chunk, n a multiple of N) must be accepted; no
+// buffers are replayed (they would be GiB).
+static void fuzz_sizing(int iters) {
+    const int Cs[] = {256, 1024, 2048};
+    const int deads[] = {0, 32, 200};
+    const int64_t trig_slots = 256 * 4 * 4, svf_lanes = 256 * 128;
+    for (int it = 0; it < iters; ++it) {
+        mkid_cfg cfg{};
+        cfg.n_channels = Cs[rint_(0, 2)];
+        cfg.fft_len = 2 * cfg.n_channels;
+        const int C = cfg.n_channels, N = cfg.fft_len;
+        cfg.pfb_taps = 4;
+        cfg.fir_taps = 26;
+        cfg.dds_entries = 65536 / C;
+        cfg.dead_time = deads[rint_(0, 2)];
+        cfg.max_events_per_ch = rint_(0, 1) ? 0 : (int)rint_(1, 5000);
+        const int64_t rows_max = rint_(1, ((int64_t)1 << rint_(20, 31)) / N);
+        cfg.max_chunk = rows_max * N;
+        const bool fused = rint_(0, 1) == 1;
+        Workspace ws;
+        const char* e = size_workspace(cfg, fused, trig_slots, svf_lanes, kSvfW, ws);
+        CHECK(e == nullptr, "size_workspace failed at max_chunk %lld: %s", (long long)cfg.max_chunk, e);
+        if (e) continue;
+        for (int call = 0; call < 8; ++call) {
+            const int mode = call % 3;
+            const int64_t rows = call < 3 ? rows_max : rint_(1, rows_max);
+            std::vector<SubPlan> subs;
+            int32_t stride = 0, capseg = 0;
+            const char* pe = plan_call(ws, C, N, mode, cfg.dead_time, rows * N, subs, stride, capseg);
+            CHECK(pe == nullptr, "legal call refused: %s (C %d rows %lld of %lld, mode %d, dead %d)", pe, C,
+                  (long long)rows, (long long)rows_max, mode, cfg.dead_time);
+            if (pe) continue;
+            CHECK((int64_t)C * stride * capseg <= ws.slot_cap && capseg <= ws.scratch_cap, "tables");
+        }
+    }
+}
+
 // seg_capacity is a hard bound: the oracle trigger, driven to fire as often as it can, never puts
 // more than seg_capacity(L, dead) packets of a channel into any window of L rows
 static void fuzz_capacity(int iters) {
@@ -269,6 +309,7 @@ int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 300;
     rng.seed(argc > 2 ? strtoull(argv[2], nullptr, 10) : 12345);
     fuzz_plans(iters);
+    fuzz_sizing(iters / 2 + 1);
     fuzz_capacity(iters / 3 + 1);
     fuzz_slot_order(iters / 10 + 2);
     fuzz_quantize(iters / 3 + 1);

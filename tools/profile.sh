@@ -8,6 +8,11 @@
 set -euo pipefail
 TAG=${1:-run}
 shift || true
+# one profiled rank per invocation: bench.py --gpus N > 1 would start its ranks from a process the
+# profiler's preloaded library has already attached to the GPU
+for a in "$@"; do
+    if [ "$a" = "--gpus" ]; then echo "profile.sh: profile one rank (no --gpus)" >&2; exit 2; fi
+done
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"

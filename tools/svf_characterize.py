@@ -8,7 +8,7 @@ on a quiet block. Every packet is matched to the last pulse of its channel that 
 before it (bench.py's window: -2 .. +60 rows); the unmatched ones are histogrammed by their delay
 after that pulse and by the pulse's amplitude, and the baseline e = f - B at the packet is kept.
 
-    python tools/svf_characterize.py [--rows 400000] [--channels 64] > profiles/r03_svf_unmatched.json
+    python tools/svf_characterize.py [--rows 400000] [--channels 64] > profiles/r03/r03_svf_unmatched.json
     python tools/svf_characterize.py --rearm 0,64,128,192,256   # re-arm hysteresis (mkid_set_rearm)
 
 Round 5 adds the re-arm level (hysteresis, mkid_set_rearm): each (mode, rearm_q8) pair reports the

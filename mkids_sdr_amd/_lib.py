@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libmkidgpu.so')
+# MKID_LIB: a build variant to test in place of the in-tree library (tools/build_variant.sh A/Bs)
+LIB_PATH = os.environ.get('MKID_LIB') or os.path.join(HERE, 'libmkidgpu.so')
 
 MKID_OK = 0
 MKID_E_ARG = -1

@@ -277,6 +277,7 @@ def test_front2_index_maps_and_lds_layouts(N):
     assert all(ok.values()), ok
     if N == 4096:
         assert m.horner_combine_f32() < 1e-6
+        assert m.precombine_f32() < 1e-6     # k_front5's radix-2 pre-combination (round 5)
 
 
 def test_resdiff_matches_reference_restatement():

@@ -72,6 +72,43 @@ def horner_combine_f32(N=4096, seed=2):
     return float(np.abs(X - ref).max() / np.abs(ref).max())
 
 
+def precombine_f32(N=4096, seed=3):
+    """k_front5.hip (round 5): the transform wave that holds sub-FFTs r and r + 4 writes
+    P_r^s[k] = Y_r[k] + (-1)^s W_1024^k Y_{r+4}[k] (W_1024^k = W_1024^{kl + 8 la} W_16^{r'} built by
+    repeated multiplication, k = 64 r' + kl + 8 la), and the select evaluates
+    X[b] = (P_0 + t^2 P_2) + t (P_1 + t^2 P_3), t = W_N^b, s = bit 9 of b; complex64 throughout as
+    the device; returns the max error relative to max |X|."""
+    rng = np.random.default_rng(seed)
+    u = (rng.normal(size=N) + 1j * rng.normal(size=N)) * 3e4
+    Ys = [np.fft.fft(u[w::8]).astype(np.complex64) for w in range(8)]
+    k = np.arange(512)
+    base = k % 64                                   # kl + 8 la
+    w0 = np.exp(-2j * np.pi * base / 1024).astype(np.complex64)
+    w16 = np.complex64(np.exp(-2j * np.pi / 16))
+    wk = w0.copy()
+    tw = np.empty(512, np.complex64)
+    for r in range(8):                              # k = 64 r + base
+        sel = (k // 64) == r
+        tw[sel] = wk[sel]
+        wk = (wk * w16).astype(np.complex64)
+    P = {}
+    for r in range(4):
+        d = (Ys[r + 4] * tw).astype(np.complex64)
+        P[(r, 0)] = (Ys[r] + d).astype(np.complex64)
+        P[(r, 1)] = (Ys[r] - d).astype(np.complex64)
+    b = np.arange(N)
+    s = (b >> 9) & 1
+    kk = b % 512
+    t = np.exp(-2j * np.pi * b / N).astype(np.complex64)
+    t2 = (t * t).astype(np.complex64)
+    g = lambda r: np.where(s == 0, P[(r, 0)][kk], P[(r, 1)][kk])
+    xa = (g(0) + t2 * g(2)).astype(np.complex64)
+    xb = (g(1) + t2 * g(3)).astype(np.complex64)
+    X = (xa + t * xb).astype(np.complex64)
+    ref = np.fft.fft(u)
+    return float(np.abs(X - ref).max() / np.abs(ref).max())
+
+
 def _groups(width):
     """lane groups (one LDS cycle each) and bank count of an instruction (MI355X_MICROARCH.md)."""
     if width == 'r32':

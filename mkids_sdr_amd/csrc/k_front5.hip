@@ -19,9 +19,13 @@
 // LDS: ring 72 KiB + Y 72 KiB + the channels' avgIQ sums 16 KiB = 160 KiB (the twiddles are
 // computed into the transform lanes' VGPRs, and the select threads' avgIQ sums live in LDS, so
 // that three channels' low-pass state fits beside the select working set in 128 VGPRs).
-// Arithmetic (PFB int16 dot products, radix-8 sub-FFTs, Horner combine in W_N^{bin} joined by
-// W_N^{4 bin}, DDC, transposed decimating low-pass, atan2, Fix16_13) is k_front4's, except that
-// W_N^{4 bin} is rebuilt by two squarings (a few ulp); both are held to the same parity bars.
+// Arithmetic: PFB int16 dot products, radix-8 sub-FFTs, DDC (with the centring constant fused in),
+// transposed decimating low-pass, atan2, Fix16_13. The 8-way decimation combine is split (round 5):
+// the transform wave that holds sub-FFTs r and r + 4 writes their radix-2 combinations
+// P_r^s[k] = Y_r[k] + (-1)^s W_1024^k Y_{r+4}[k] (s = bit 9 of the bin), and a select thread reads
+// the 4 regions of its bin's s and evaluates X[b] = (P_0 + t^2 P_2) + t (P_1 + t^2 P_3), t = W_N^b:
+// 4 instead of 8 bin-indexed LDS reads and 4 instead of 9 complex MACs per channel-frame
+// (tools/front2_layouts.py precombine_f32, same-box -6 %, profiles/r05/r05l_kbench_c5.json).
 #include "front_common.h"
 
 #include <type_traits>
@@ -119,7 +123,8 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
         double sn, cn;
         sincospi(-2.0 * (double)bin / G5::N, &sn, &cn);
         tb[q] = make_float2((float)cn, (float)sn);
-        yoff[q] = yswz(bin & 511);
+        // P_r^s of the bin's half s = bit 9 (regions r + 4 s, r = 0..3): see the transform waves
+        yoff[q] = yswz(bin & 511) + ((bin >> 9) & 1) * 4 * G5::REG;
         ysl[c] = ACC ? make_float2(0.f, 0.f) : a.cen.ncen[c];   // the thread's own channels only
     }
     uint64_t gp[13];
@@ -174,28 +179,22 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             auto zq = [&](int q) {   // z - c' of channel slot q
                 const float2 lo = lov[q];
                 const float2* yq = yf + yoff[q];
-                // two 4-term Horner chains in W_N^{bin}, reads in two halves (8 VGPRs of reads in flight)
-                float2 Xl = yq[3 * G5::REG], Xh = yq[7 * G5::REG];
-                float2 y2 = yq[2 * G5::REG], y6 = yq[6 * G5::REG];
-                Xl = cmac(y2, Xl, tb[q]);
-                Xh = cmac(y6, Xh, tb[q]);
-                __builtin_amdgcn_sched_barrier(0);
-                const float2 y1 = yq[G5::REG], y5 = yq[5 * G5::REG], y0 = yq[0], y4 = yq[4 * G5::REG];
-                Xl = cmac(y1, Xl, tb[q]);
-                Xh = cmac(y5, Xh, tb[q]);
-                Xl = cmac(y0, Xl, tb[q]);
-                Xh = cmac(y4, Xh, tb[q]);
-                // joined by W_N^{4 bin} = (W_N^{bin})^4 (two squarings: a few ulp, far below the phase bar)
+                // X[b] = sum_r t^r P_r^s[b mod 512], t = W_N^b: (P0 + t^2 P2) + t (P1 + t^2 P3)
+                const float2 y0 = yq[0], y1 = yq[G5::REG], y2 = yq[2 * G5::REG], y3 = yq[3 * G5::REG];
                 const float2 t2 = cmul_pk(tb[q], tb[q]);
-                return cmul_add_pk(cmac(Xl, Xh, cmul_pk(t2, t2)), lo, ncv[q]);
+                const float2 xa = cmac(y0, t2, y2), xb = cmac(y1, t2, y3);
+                return cmul_add_pk(cmac(xa, tb[q], xb), lo, ncv[q]);
             };
             if (f == 0) {
+                // every channel's X first (its 4 reads in flight together), then the accumulations
+                float2 zz[CPT];
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) zz[q] = zq(q);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int q = 0; q < CPT; ++q) {
-                    const float2 z = zq(q);
 #pragma unroll
-                    for (int m = 0; m < 13; ++m) acc[q][m] = fma_tap<1>(gp[m], z, acc[q][m]);   // g_{2m+1}
-                    __builtin_amdgcn_sched_barrier(0);
+                    for (int m = 0; m < 13; ++m) acc[q][m] = fma_tap<1>(gp[m], zz[q], acc[q][m]);   // g_{2m+1}
                 }
             } else {
                 const int ko = kf + 1;   // odd: output row (ko - 1) / 2 of the run
@@ -320,6 +319,14 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
         __syncthreads();
         // the lane's stage-1 / stage-2 twiddles W_512^{L k}, W_64^{la k} (the same every frame)
         float2 w1[7], w2[7];
+        float2 w0, w16;   // W_1024^{kl + 8 la} and W_1024^64 = W_16 (the pre-combination twiddles)
+        {
+            double sn, cn;
+            sincospi(-2.0 * (double)(kl + 8 * la) / 1024.0, &sn, &cn);
+            w0 = make_float2((float)cn, (float)sn);
+            sincospi(-2.0 / 16.0, &sn, &cn);
+            w16 = make_float2((float)cn, (float)sn);
+        }
 #pragma unroll
         for (int k = 1; k < 8; ++k) {
             double sn, cn;
@@ -387,8 +394,24 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
                     dft<8>(v);
                     __builtin_amdgcn_wave_barrier();
                     float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
+                    if (s == 0) {
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
+                        for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];   // Y_rw, combined below
+                    } else {
+                        // radix-2 pre-combination of this wave's two sub-FFTs (w = rw + 4):
+                        //   P_rw^s[k] = Y_rw[k] + (-1)^s W_1024^k Y_{rw+4}[k],  k = 64 r + kl + 8 la
+                        // (W_N^{4b} = W_1024^k (-1)^{b >> 9}), so a select reads 4 regions, not 8
+                        float2* yw0 = fb + rw * G::REG + ((kl + 8 * la) ^ (la << 1));
+                        float2 wk = w0;
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const float2 y0 = yw0[64 * r];
+                            const float2 d = cmul_pk(v[r], wk);
+                            yw0[64 * r] = make_float2(y0.x + d.x, y0.y + d.y);
+                            yw[64 * r] = make_float2(y0.x - d.x, y0.y - d.y);
+                            if (r < 7) wk = cmul_pk(wk, w16);
+                        }
+                    }
                     STAMP5(t, 1 + s);
                 }
                 // ring refill: hop k + 1 over hop k - 2T (read by no one in this iteration)

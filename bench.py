@@ -164,11 +164,14 @@ def make_pulses(C, n_samples, N, rate, rng):
     return s[o], np.concatenate(tones)[o], np.concatenate(amps)[o]
 
 
-def detector_score(ev, j_last, ps, pt, N, early=2, late=60, isolation=400):
+def detector_score(ev, j_last, ps, pt, N, early=2, late=60, isolation=400, atten=None, loop_R=None):
     """Packets of the last step against the injected pulses (start sample ps, channel pt): a packet
     of channel c at row r matches a pulse of c starting at row p when p - early <= r <= p + late.
     Returns the fraction of isolated pulses (no other pulse of the channel within `isolation`
-    rows) with exactly one packet, and the packets matching no pulse."""
+    rows) with exactly one packet, and the packets matching no pulse, histogrammed by their delay
+    after the channel's previous pulse (a tail re-fire sits 60-300 rows after it, a noise trigger
+    anywhere) and, given the per-channel attenuations and loop fractions R (loop radius over the
+    tone's distance from the origin), by the channel's attenuation and R."""
     ev = np.asarray(ev, np.uint64)
     ch = ((ev >> np.uint64(52)) & np.uint64(0xFFF)).astype(np.int64)
     row = ((ev & np.uint64((1 << 28) - 1)).astype(np.int64) - j_last) % (1 << 28)
@@ -184,9 +187,28 @@ def detector_score(ev, j_last, ps, pt, N, early=2, late=60, isolation=400):
     same_prev = np.r_[False, pch[1:] == pch[:-1]] & (np.r_[0, np.diff(prow)] < isolation)
     same_next = np.r_[pch[1:] == pch[:-1], False] & (np.r_[np.diff(prow), 0] < isolation)
     iso = ~(same_prev | same_next)
-    return dict(isolated=int(iso.sum()), exactly_one_frac=round(float((nhit[iso] == 1).mean()), 4) if iso.any() else None,
-                missed=int((nhit[iso] == 0).sum()), multi=int((nhit[iso] > 1).sum()),
-                unmatched_packets=int((~ok).sum()), packets=int(len(ev)))
+    um = ~ok
+    prev = (k >= 0) & (pch[np.maximum(k, 0)] == ch)
+    delay = np.where(prev, row - prow[np.maximum(k, 0)], -1)[um]
+    edges = [61, 100, 200, 300, 1000, 1 << 40]
+    hist = {'no_earlier_pulse': int((delay < 0).sum())}
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        hist['%d-%s' % (lo, hi - 1 if hi < (1 << 40) else 'inf')] = int(((delay >= lo) & (delay < hi)).sum())
+    out = dict(isolated=int(iso.sum()), exactly_one_frac=round(float((nhit[iso] == 1).mean()), 4) if iso.any() else None,
+               missed=int((nhit[iso] == 0).sum()), multi=int((nhit[iso] > 1).sum()),
+               unmatched_packets=int(um.sum()), packets=int(len(ev)), pulses=int(len(key)),
+               unmatched_per_pulse=round(float(um.sum()) / max(1, len(key)), 5),
+               unmatched_delay_rows=hist)
+    if atten is not None and um.any():
+        a = np.asarray(atten, np.float64)[ch[um]]
+        out['unmatched_by_atten_db'] = [{'atten_db': [lo, lo + 5], 'packets': int(((a >= lo) & (a < lo + 5)).sum())}
+                                        for lo in range(0, int(np.ceil(a.max() + 1e-9)) + 1, 5)
+                                        if ((a >= lo) & (a < lo + 5)).any()]
+    if loop_R is not None and um.any():
+        r = np.asarray(loop_R, np.float64)[ch[um]]
+        out['unmatched_by_loop_R'] = [{'R': [lo, hi], 'packets': int(((r >= lo) & (r < hi)).sum())}
+                                      for lo, hi in ((0.0, 0.25), (0.25, 0.5), (0.5, 0.75), (0.75, 1.01))]
+    return out
 
 
 def pulse_filter(C, npre=20, ncoeff=100, tau_fall=65.0):
@@ -518,7 +540,8 @@ def main():
     det = None
     if rank == 0:
         det = detector_score(d_events[:int(counts[1])].cpu().numpy().view(np.uint64),
-                             (args.warmup + args.steps - 1) * J, ps, pt, N)
+                             (args.warmup + args.steps - 1) * J, ps, pt, N,
+                             atten=feed['attens'], loop_R=feed['loop_R'])
     reruns = ch.trigger_reruns()
     ch.set_timing(False)
     # N > 1: every rank's own feedline gets a parity witness: the first

@@ -65,8 +65,8 @@ def parse():
     p.add_argument('--config', type=int, default=3, choices=sorted(CONFIGS))
     p.add_argument('--baseline', default='ema', choices=['ema', 'svf'])
     p.add_argument('--rearm-q8', type=int, default=None,
-                   help='trigger re-arm hysteresis /256 (mkid_set_rearm); default 32 for svf (removes the '
-                        'pulse-tail re-fires, tools/svf_characterize.py), 0 for ema')
+                   help='trigger re-arm hysteresis /256 (mkid_set_rearm); default 96 for svf (removes the '
+                        'pulse-tail re-fires on the operating-condition stream, DESIGN.md §2), 0 for ema')
     p.add_argument('--log2-samples', type=int, default=None, help='override the config sample count')
     p.add_argument('--pulse-rate', type=float, default=1.0 / 2048,
                    help='Poisson pulses per phase sample per channel')
@@ -400,7 +400,7 @@ def main():
     ch.set_fir(np.tile(mf, (C, 1)))
     ch.set_baseline(base_mode, 41, 82, 93623, 8192)
     if args.rearm_q8 is None:
-        args.rearm_q8 = 32 if args.baseline == 'svf' else 0
+        args.rearm_q8 = 96 if args.baseline == 'svf' else 0
     ch.set_rearm(args.rearm_q8)
 
     # ---- synthetic input resident in HBM ----

@@ -25,7 +25,7 @@
 // P_r^s[k] = Y_r[k] + (-1)^s W_1024^k Y_{r+4}[k] (s = bit 9 of the bin), and a select thread reads
 // the 4 regions of its bin's s and evaluates X[b] = (P_0 + t^2 P_2) + t (P_1 + t^2 P_3), t = W_N^b:
 // 4 instead of 8 bin-indexed LDS reads and 4 instead of 9 complex MACs per channel-frame
-// (tools/front2_layouts.py precombine_f32, same-box -6 %, profiles/r05/r05l_kbench_c5.json).
+// (tools/front2_layouts.py precombine_f32, same-box -6 %, profiles/r05/r05l_kbench_c5_precombine.json).
 #include "front_common.h"
 
 #include <type_traits>

@@ -12,8 +12,9 @@
 //     (c = st + 512 q), waves 12-15 two (c = 1536 + st' + 256 q), so every SIMD carries one
 //     transform wave and select work for 512 channels;
 //   * one frame per iteration (the LDS does not hold two frames' Y twice at N = 4096): ring of
-//     2T + 1 = 9 hops (frame k reads hops k-7 .. k, the transform waves write the prefetched hop
-//     k + 1 over hop k - 8), Y [2][8][576] float2, one workgroup barrier per frame;
+//     2T + 1 = 9 hops (frame k reads hops k-7 .. k; select waves 12-15 load hop k + 1 and write it
+//     over hop k - 8 in the same barrier interval, off the transform chain), Y [2][8][576] float2,
+//     one workgroup barrier per frame;
 //   * the select threads' state lives in registers only in the select waves, so the 13 complex
 //     low-pass accumulators of three channels (78 VGPRs) no longer share the file with the FFT.
 // LDS: ring 72 KiB + Y 72 KiB + the channels' avgIQ sums 16 KiB = 160 KiB (the twiddles are
@@ -110,9 +111,15 @@ __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 
 // Registers go to the low-pass state: the centring constants (mkid_internal.h Centring) are re-read
 // per frame, -c' from the per-channel LDS slot ysl (ACC = false) or, while the avgIQ accumulator
 // is armed and ysl holds its partial sums (ACC = true), from global memory; r at output frames.
-template <int CPT, bool ACC>
+// RF (waves 12-15, 256 threads like the transform waves, the lightest select work): the ring
+// refill. In the barrier interval in which the transform waves compute frame k (one ahead of the
+// select), hop k + 1 goes over hop k - 2T, a slot no wave reads in that interval; thread xt loads
+// and writes the 8 samples load_hop / ring_put give it. Off the transform waves' chain: -8.8 %
+// same box (profiles/r05/r05u_kbench_c5_refill.json; waves 4-7 or 4-11 instead: -7 %).
+template <int CPT, bool ACC, bool RF>
 __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0, int cs,
-                                           int64_t k_b, int64_t k_start, int nrun, int nit) {
+                                           int64_t k_b, int64_t k_start, int nrun, int nit, uint32_t* ring, int xt) {
+    constexpr int RS = G5::RS;
     constexpr int C = G5::C;
     float2 tb[CPT];   // W_N^{bin}
     int yoff[CPT];
@@ -139,6 +146,12 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
     float* const phase_run = a.phase ? a.phase + (k_b >> 1) * C : nullptr;
     int lrow = (int)((a.k0 + k_start) & (int64_t)(a.P - 1));
     __syncthreads();   // prologue: ring written
+    if (RF) {          // transform iteration 0 computes frame k_start: hop k_start + 1
+        uint4 v0, v1;
+        const int64_t h = k_start + 1;
+        load_hop(a, h, xt, v0, v1);
+        ring_put(ring + (int)(((h % RS) + RS) % RS) * G5::M, xt, v0, v1);
+    }
     __syncthreads();   // transform iteration 0 (frame k_start) wrote Y buffer 0
     // frames in pairs (even: accumulate, odd: output), one barrier after each: frame k_start + 2p
     // is in Y buffer 0, k_start + 2p + 1 in buffer 1 (nit is even). Unrolled by hand so the
@@ -152,6 +165,12 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
             STAMP5(2 * p + 1 + f, 8);
+            // this interval's refill (transform iteration 2p + f + 1, frame k_start + 2p + f + 1):
+            // hop k_start + 2p + f + 2, loaded first (its wait then covers nothing issued later)
+            const int64_t hr = k_start + 2 * p + f + 2;
+            const bool rf = RF && 2 * p + f + 1 < nit;
+            uint4 rv0, rv1;
+            if (rf) load_hop(a, hr, xt, rv0, rv1);
             // channel base re-defined every frame so per-channel addresses are rebuilt in the loop
             // (a few VALU) instead of being hoisted as 64-bit pointers that crowd the low-pass state
             int cb = c0;
@@ -252,6 +271,7 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                     if (iqhit) *reinterpret_cast<uint32_t*>(a.iqtap + 2 * ((k_b >> 1) + jr)) = iqv;
                 }
             }
+            if (rf) ring_put(ring + (int)(((hr % RS) + RS) % RS) * G5::M, xt, rv0, rv1);
             STAMP5(2 * p + 1 + f, 9);
             __syncthreads();   // Y buffer f read; the transform waves wrote the next frame into 1 - f
             STAMP5(2 * p + 1 + f, 10);
@@ -339,10 +359,6 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
         for (int t = 0; t <= nit; ++t) {
             STAMP5(t, 0);
             if (t < nit) {
-                const int kr = -kLpfHist + t;
-                // the hop iteration t + 1 adds: loaded now, written after this wave's PFB reads
-                uint4 pre0, pre1;
-                load_hop(a, k_b + kr + 1, xt, pre0, pre1);
                 float2* fb = fbuf + (t & 1) * G::FB;
 #pragma unroll
                 for (int s = 0; s < G::SPW; ++s) {
@@ -414,10 +430,7 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
                     }
                     STAMP5(t, 1 + s);
                 }
-                // ring refill: hop k + 1 over hop k - 2T (read by no one in this iteration)
-                int ws = rb + 2 * T;
-                ws -= ws >= RS ? RS : 0;
-                ring_put(ring + ws * M, xt, pre0, pre1);
+                // the ring refill (hop k + 1 over hop k - 2T) is done by select waves 12-15
                 rb += 1;
                 rb -= rb >= RS ? RS : 0;
             }
@@ -432,9 +445,10 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
         // ---------------- select waves, one frame behind the transform waves --------------------
         const int sw = wave - G::FW;
         if (sw < G::SW3)
-            select_run<3, ACC>(a, fbuf, ysl, sw * 64 + L, 512, k_b, k_start, nrun, nit);
+            select_run<3, ACC, false>(a, fbuf, ysl, sw * 64 + L, 512, k_b, k_start, nrun, nit, ring, 0);
         else
-            select_run<2, ACC>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64 + L, 256, k_b, k_start, nrun, nit);
+            select_run<2, ACC, true>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64 + L, 256, k_b, k_start, nrun, nit,
+                                     ring, tid - (G::FW + G::SW3) * 64);
     }
 }
 

@@ -157,6 +157,10 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
         uint2 tq[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
+        // the taps are complete before the loop: otherwise the loop's waits on them (vmcnt counts
+        // retire in order) also wait on each iteration's ring prefetch, exposing its HBM latency
+#pragma unroll
+        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(tq[r].x), "+v"(tq[r].y));
         const int la = L & 7, kl = L >> 3;
         const float2* t1 = tw1 + L;
         const float2* t2 = tw2 + la;

@@ -360,6 +360,10 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
             STAMP5(t, 0);
             if (t < nit) {
                 float2* fb = fbuf + (t & 1) * G::FB;
+                // Y_rw of sub-FFT 0, held in VGPRs for the pre-combination (16 VGPRs the transform
+                // path has since the ring refill left it; -3 % against its LDS write + read-back,
+                // profiles/r05/r05z_kbench_c5_yreg.json)
+                float2 yr[8];
 #pragma unroll
                 for (int s = 0; s < G::SPW; ++s) {
                     const int w = rw + G::FW * s;
@@ -412,7 +416,7 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
                     float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
                     if (s == 0) {
 #pragma unroll
-                        for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];   // Y_rw, combined below
+                        for (int r = 0; r < 8; ++r) yr[r] = v[r];   // Y_rw, combined below
                     } else {
                         // radix-2 pre-combination of this wave's two sub-FFTs (w = rw + 4):
                         //   P_rw^s[k] = Y_rw[k] + (-1)^s W_1024^k Y_{rw+4}[k],  k = 64 r + kl + 8 la
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
                         float2 wk = w0;
 #pragma unroll
                         for (int r = 0; r < 8; ++r) {
-                            const float2 y0 = yw0[64 * r];
+                            const float2 y0 = yr[r];
                             const float2 d = cmul_pk(v[r], wk);
                             yw0[64 * r] = make_float2(y0.x + d.x, y0.y + d.y);
                             yw[64 * r] = make_float2(y0.x - d.x, y0.y - d.y);

@@ -9,7 +9,7 @@ namespace {
 // k_front3 ring plane layout (NW = 4, Q = 256 samples per plane): samples qoff..qoff+3 of a hop go
 // to planes 0..3 at plane index qoff / 4, paired (ring3_idx). The refill's ds_write_b32 become
 // 2-way bank conflicts, which cost no extra cycles for ds_write_b32 (MI355X_MICROARCH.md §LDS).
-__device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
+[[maybe_unused]] __device__ __forceinline__ void ring3_put(uint32_t* hop, int qoff, uint4 v) {
     constexpr int Q = 256;
     const int a = ring3_idx(qoff / 4);
     hop[a] = v.x;
@@ -379,6 +379,28 @@ static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifdef MKID_F3_N
+// One geometry per object (Makefile: k_front3_<N>.o), so that each takes scheduler flags of its
+// own (F3_FLAGS_<N>); the N = 2048 object also holds the dispatch.
+hipError_t launch_front3_512(const FrontArgs& a, hipStream_t s);
+hipError_t launch_front3_1024(const FrontArgs& a, hipStream_t s);
+hipError_t launch_front3_2048(const FrontArgs& a, hipStream_t s);
+#define MKID_F3_CAT2(a, b) a##b
+#define MKID_F3_CAT(a, b) MKID_F3_CAT2(a, b)
+hipError_t MKID_F3_CAT(launch_front3_, MKID_F3_N)(const FrontArgs& a, hipStream_t s) {
+    return launch_front3_n<MKID_F3_N>(a, s);
+}
+#if MKID_F3_N == 2048
+hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s) {
+    switch (N) {
+        case 2048: return launch_front3_2048(a, s);
+        case 1024: return launch_front3_1024(a, s);
+        case 512: return launch_front3_512(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+#endif
+#else
 hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s) {
     switch (N) {
         case 2048: return launch_front3_n<2048>(a, s);
@@ -387,5 +409,6 @@ hipError_t launch_front3(int N, const FrontArgs& a, hipStream_t s) {
         default: return hipErrorInvalidValue;
     }
 }
+#endif
 
 }  // namespace mkid

@@ -159,8 +159,12 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
         for (int r = 0; r < 8; ++r) tq[r] = a.pfbq[NW * (64 * r + L) + w];
         // the taps are complete before the loop: otherwise the loop's waits on them (vmcnt counts
         // retire in order) also wait on each iteration's ring prefetch, exposing its HBM latency
+        // (N = 1024: -3.6 %; N = 512, scheduled max-ILP: +3 %, left to the scheduler there;
+        // profiles/r05/r05al_kbench_{c2,512}_tq.json)
+        if constexpr (N != 512) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(tq[r].x), "+v"(tq[r].y));
+            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(tq[r].x), "+v"(tq[r].y));
+        }
         const int la = L & 7, kl = L >> 3;
         const float2* t1 = tw1 + L;
         const float2* t2 = tw2 + la;

@@ -97,12 +97,15 @@ int mkid_set_stream(mkid_ctx* ctx, void* hip_stream);
 int mkid_set_pfb(mkid_ctx* ctx, const float* coeffs, int32_t n);
 /* Host-only (no device needed): the effective taps h_q * 2^-S of mkid_set_pfb and S. */
 int mkid_pfb_effective_taps(const float* coeffs, int32_t T, int32_t N, float* out, int32_t* shift);
-/* Host-only: the channel order the N = 2048 front end (k_front3) gives its select threads for a
- * bin set (the C = 2048 order of the same scheme is reported too, unused by k_front5): out[st + (C/2) q] = channel read by thread st in instruction q.
- * Each wave keeps its own 128 channels; within them the order puts each half-wave's 32 Y reads on
- * distinct LDS bank pairs where the bins allow. A permutation of 0..C-1 (the identity for C other
- * than 1024 and 2048). Results do not depend on it: each channel's arithmetic is unchanged.
- * Exposed for tests and tools/lds_assign.py; MKID_SLOT_ORDER=0 at context creation disables it. */
+/* Host-only: the channel order the fused front ends give their select threads for a bin set:
+ * out[slot] = channel. C = 1024 (k_front3, N = 2048): slot st + 512 q is read by thread st in
+ * instruction q, and each select wave keeps its own 128 channels. C = 2048 (k_front5, N = 4096):
+ * slot 64 sw + l + 512 q (select waves sw < 8, q < 3) or 1536 + 64 v + l + 256 q (v < 4, q < 2),
+ * each wave keeping the natural channels of its slots. Within a wave the order puts each
+ * half-wave's 32 Y reads on distinct LDS bank pairs where the bins allow. A permutation of 0..C-1
+ * (the identity for C other than 1024 and 2048). Results do not depend on it: each channel's
+ * arithmetic is unchanged. Exposed for tests and tools/lds_assign.py; MKID_SLOT_ORDER=0 at context
+ * creation disables it. */
 int mkid_slot_order(const int32_t* bins, int32_t C, int16_t* out);
 
 /* Coarse FFT bin per channel: replaces write_int('bins'), write_int('load_bins',(i<<1)+1)
@@ -200,14 +203,16 @@ int mkid_read_iq_tap(mkid_ctx* ctx, int16_t* host_iq, int64_t cap_rows, int64_t*
 int mkid_trigger_reruns(mkid_ctx* ctx, int64_t* total);
 
 /* avgIQ accumulator (K9): replaces startAccumulator / avgIQ_ctrl (ROACH_Setup.py:654-659,
- * rotateLoopsReady). enable = 1 arms it — the sums restart (the avgIQ_ctrl strobe) and every
+ * rotateLoopsReady). enable = 1 arms it — the sums restart on every call with 1, armed or not
+ * (the avgIQ_ctrl strobe the reference writes before each startAccumulator 1) — and every
  * following process call adds its rows; 0 stops it and keeps the sums. Off after mkid_create; the
  * front ends skip the accumulation while it is off. mkid_reset_stream clears the sums and keeps
  * the armed state. */
 int mkid_set_accumulator(mkid_ctx* ctx, int32_t enable);
 /* Per-channel mean I/Q (low-pass output y, ADC-count units) over the rows accumulated since the
  * accumulator was last armed (avgIQ_bram, ROACH_Setup.py:654-662), [C] each. MKID_E_STATE when it
- * holds no rows. */
+ * holds no rows, or when a process call failed while it was armed (its sums may hold part of that
+ * call; re-arm to start a new average). */
 int mkid_avg_iq(mkid_ctx* ctx, float* mean_i, float* mean_q);
 
 /* Re-encode wide device packets as the reference 64-bit packet (host memory, C <= 254):

@@ -212,6 +212,12 @@ def encode_conv_phase_snap(raw):
     return a.tobytes()
 
 
+def decode_conv_phase_snap(buf):
+    """conv_phase_snap{I,Q,Phase}_bram: the '>h' sample in bytes [2:4] of every 32-bit word
+    (readouttesterIQ.py:71-74, ROACH_Pulses_IQ.py:404-406, pulse_triggering_v2.py:93-94)."""
+    return np.frombuffer(buf, '>i2').reshape(-1, 2)[:, 1].astype(np.int64)
+
+
 def encode_iq_snap(I, Q):
     """conv_phase_snapIQ_bram: 16 bytes per 2 I/Q pairs, I nibble-straddled over bytes 6-8 / 11-13,
     Q in bytes 9-10 / 14-15 (pulse_triggering_IQ.py:133-147)."""

@@ -1,4 +1,4 @@
-// Helpers shared by the fused front ends (k_front2.hip, k_front3.hip, k_front4.hip, k_front5.hip):
+// Helpers shared by the fused front ends (k_front3.hip, k_front5.hip):
 // the exact int16 PFB dot product, the 512-point sub-FFT's in-wave LDS transpose and Y swizzle,
 // the paired ring-plane index, and the 16-byte hop loader.
 #pragma once
@@ -34,7 +34,7 @@ __device__ __forceinline__ int ring3_idx(int i) { return 128 * (i >> 7) + 2 * (i
 // entries; reads: entries 8 (r + r') + la mod 32 distinct over a lane group, r = L' >> 3 < 4
 // there), every offset an immediate. 8 writes + 8 reads replace 32 VALU cross-lane moves (DPP
 // row_ror:8 + v_permlane16/32_swap), which cost more on VALU-issue-bound transform waves
-// (-3.9 % k_front3, -5.3 % k_front2 at N = 512, -1.6 % k_front4: DESIGN.md §5).
+// (-3.9 % k_front3 at N = 2048, round 3: DESIGN.md §5.2).
 __device__ __forceinline__ void t1_lds(float2 (&v)[8], float2* reg, int L) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) reg[72 * r + L] = v[r];

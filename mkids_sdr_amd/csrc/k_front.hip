@@ -353,9 +353,7 @@ __global__ __launch_bounds__(FGeo<N>::BT, FGeo<N>::MINW) void k_front(FrontArgs 
 bool fused_supported(int N) { return N == 128 || N == 256 || N == 512 || N == 1024 || N == 2048 || N == 4096; }
 
 // the fused front end of each FFT length: k_front (this file) at N = 128 / 256, the
-// wave-specialised k_front3 at 512 / 1024 / 2048 and k_front5 at 4096 (round 5 retired k_front2
-// and k_front4: k_front3 measured -5.3 % at N = 512 and -10.7 % at N = 1024 against k_front2,
-// k_front5 -12.7 % against k_front4, same-box A/Bs in profiles/)
+// wave-specialised k_front3 at 512 / 1024 / 2048 and k_front5 at 4096
 hipError_t launch_fused(int N, const FrontArgs& a, hipStream_t s) {
     if (N == 4096) return launch_front5(a, s);
     if (N >= 512) return launch_front3(N, a, s);

@@ -1,6 +1,6 @@
-// Fused front end k_front3 (the default at N = 2048, config 3/4, and since round 4 at N = 512,
-// config 2: -5.3 % same-box, profiles/r04/r04_k_kbench_f3_512_vs_f2.json): k_front2's arithmetic
-// (k_front2.hip) with wave specialisation.
+// Fused front end k_front3, the default at N = 512 / 1024 / 2048 (configs 2, 3/4): the PFB, the
+// in-wave 512-point sub-FFTs, the bin-select combine, DDC, low-pass and phase, with the waves of a
+// workgroup specialised into transform and select roles.
 #include "front_common.h"
 
 namespace mkid {
@@ -18,10 +18,9 @@ namespace {
     hop[3 * Q + a] = v.w;
 }
 }  // namespace
-// In k_front2 every wave runs the FFT phase, then every wave runs the select phase, with a
-// workgroup barrier between them: when all four waves of a SIMD wait on LDS (ring reads, the
-// select's bin-indexed reads) or on a barrier, the SIMD idles (stamps: the FFT phase of the last
-// wave of a SIMD ends ~2.4k cycles after the first, VALU busy ~70 %). Here waves 0-7 only transform
+// Why specialise: when every wave runs the FFT phase and then the select phase with a barrier
+// between them (the round-2 design, history in DESIGN.md Appendix A), a SIMD idles whenever all its
+// waves wait on LDS (ring reads, the select's bin-indexed reads) or on the barrier. Here waves 0-7 only transform
 // (2 frames per iteration, one 512-point sub-FFT each) and waves 8-15 only select / mix / low-pass /
 // phase (two channels per thread), one iteration behind, on a double-buffered Y: each SIMD holds
 // two FFT and two select waves whose LDS waits and VALU bursts interleave, one barrier per
@@ -40,7 +39,7 @@ namespace {
 // 768-thread workgroups per CU at one frame per iteration (k_front6, +25 %), commit ac8fe74.
 
 // Geometry per N. N = 2048 (config 3/4): 8 transform waves (4 sub-FFTs x 2 frames) + 8 select
-// waves (2 channels per thread), one workgroup per CU. N = 1024 (round 5, replacing k_front2): 8
+// waves (2 channels per thread), one workgroup per CU. N = 1024 (round 5): 8
 // transform waves (2 sub-FFTs x 4 frames) + 8 select waves (1 channel per thread), one workgroup
 // per CU. N = 512 (config 2, round 4): 4 transform waves (the 512-point FFT of each of 4 frames) +
 // 4 select waves (1 channel per thread), two workgroups per CU.
@@ -374,7 +373,7 @@ static hipError_t launch_front3_n(const FrontArgs& a0, hipStream_t s) {
     FrontArgs a = a0;
     if (a.K <= 0) return hipSuccess;
     const int64_t ncu = a.ncu > 0 ? a.ncu : 256;
-    int64_t fpb = a.K / (ncu * G::WG_PER_CU);    // one run per resident workgroup, as k_front2
+    int64_t fpb = a.K / (ncu * G::WG_PER_CU);    // one run per resident workgroup
     fpb = fpb < 64 ? 64 : (fpb > 4096 ? 4096 : fpb);
     fpb = (fpb + G::F - 1) / G::F * G::F;
     a.frames_per_block = fpb;

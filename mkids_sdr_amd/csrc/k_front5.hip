@@ -1,10 +1,10 @@
 // k_front5: the fused front end for N = 4096 (2048 channels, BASELINE config 5) with WAVE
-// SPECIALISATION, the k_front3 scheme (k_front2.hip) re-fitted to a 4096-point frame.
+// SPECIALISATION, the k_front3 scheme re-fitted to a 4096-point frame.
 //
-// k_front4 runs every wave through both phases of an iteration (PFB + sub-FFTs, barrier, select /
-// DDC / low-pass / phase, barrier) and keeps the FFT working set and two channels' low-pass state
-// live together in 128 VGPRs (17-21 dwords spilled); stamps show the SIMDs idling through both
-// barrier phases (VALU active 45 %). Here the two phases run in different waves, one iteration
+// Running every wave through both phases of an iteration (PFB + sub-FFTs, barrier, select / DDC /
+// low-pass / phase, barrier; the round-2 design) keeps the FFT working set
+// and two channels' low-pass state live together in 128 VGPRs (17-21 dwords spilled) and idles the
+// SIMDs through both barrier phases (VALU active 45 %). Here the two phases run in different waves, one iteration
 // apart, so each SIMD always holds waves of both kinds:
 //   * waves 0-3 transform: wave r computes sub-FFTs r and r + 4 (512 points each, in-wave, as in
 //     k_front3) of frame k and writes them to Y buffer t & 1;
@@ -95,7 +95,7 @@ __device__ __forceinline__ void load_hop(const FrontArgs& a, int64_t hop, int xt
 }
 
 // hop layout: sample o at plane o % 8, plane index o / 8 stored at ring3_idx(o / 8), the paired
-// plane layout of k_front3 / k_front4 (plane entries 64 apart adjacent, so a lane's PFB points
+// plane layout of k_front3 (plane entries 64 apart adjacent, so a lane's PFB points
 // r, r + 1 are one ds_read_b64)
 __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 v1) {
     constexpr int Q = G5::Q;
@@ -107,7 +107,11 @@ __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 
 // measured and dropped (DESIGN.md §5 k_front5): T1 in registers, LO one frame ahead, one Horner
 // chain, even/odd chains, unsplit Y reads, no barrier between channels, transform-wave priority
 
-// select / DDC / low-pass / phase of CPT channels c0 + cs q per thread, frame k - 1 of iteration t.
+// select / DDC / low-pass / phase of the CPT channels of select slots c0 + cs q (c0 = c0w + lane),
+// frame k - 1 of iteration t. Slot -> channel is the host's bank-aware order (mkid_plan.cpp
+// slot_order, a.slot_ch; nullptr: identity): each wave keeps its own channels, c0w + l + cs q'
+// (l < 64), so a thread packs its channels as 8-bit (q', l) codes in one VGPR and rebuilds them per
+// frame; the per-channel LDS slot ysl is indexed by SLOT (lane-consecutive, conflict-free).
 // Registers go to the low-pass state: the centring constants (mkid_internal.h Centring) are re-read
 // per frame, -c' from the per-channel LDS slot ysl (ACC = false) or, while the avgIQ accumulator
 // is armed and ysl holds its partial sums (ACC = true), from global memory; r at output frames.
@@ -117,22 +121,25 @@ __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 
 // and writes the 8 samples load_hop / ring_put give it. Off the transform waves' chain: -8.8 %
 // same box (profiles/r05/r05u_kbench_c5_refill.json; waves 4-7 or 4-11 instead: -7 %).
 template <int CPT, bool ACC, bool RF>
-__device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0, int cs,
+__device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0w, int cs,
                                            int64_t k_b, int64_t k_start, int nrun, int nit, uint32_t* ring, int xt) {
     constexpr int RS = G5::RS;
     constexpr int C = G5::C;
     float2 tb[CPT];   // W_N^{bin}
     int yoff[CPT];
+    const int c0 = c0w + (int)(threadIdx.x & 63);
+    uint32_t pk = 0;  // channel of slot q: c0w + (pk >> 8q & 63) + cs (pk >> (8q + 6) & 3)
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
-        const int c = c0 + cs * q;
+        const int c = a.slot_ch ? (int)a.slot_ch[c0 + cs * q] : c0 + cs * q;
+        pk |= (uint32_t)((((c - c0w) / cs) << 6) | ((c - c0w) & 63)) << (8 * q);
         const int32_t bin = a.bins[c];
         double sn, cn;
         sincospi(-2.0 * (double)bin / G5::N, &sn, &cn);
         tb[q] = make_float2((float)cn, (float)sn);
         // P_r^s of the bin's half s = bit 9 (regions r + 4 s, r = 0..3): see the transform waves
         yoff[q] = yswz(bin & 511) + ((bin >> 9) & 1) * 4 * G5::REG;
-        ysl[c] = ACC ? make_float2(0.f, 0.f) : a.cen.ncen[c];   // the thread's own channels only
+        ysl[c0 + cs * q] = ACC ? make_float2(0.f, 0.f) : a.cen.ncen[c];   // the thread's own slots only
     }
     uint64_t gp[13];
 #pragma unroll
@@ -171,10 +178,17 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             const bool rf = RF && 2 * p + f + 1 < nit;
             uint4 rv0, rv1;
             if (rf) load_hop(a, hr, xt, rv0, rv1);
-            // channel base re-defined every frame so per-channel addresses are rebuilt in the loop
-            // (a few VALU) instead of being hoisted as 64-bit pointers that crowd the low-pass state
-            int cb = c0;
-            asm volatile("" : "+v"(cb));
+            // slot base and channel codes re-defined every frame so per-channel addresses are rebuilt
+            // in the loop (a few VALU) instead of being hoisted as 64-bit pointers that crowd the
+            // low-pass state
+            int lane;   // the slot base from the lane id, recomputed here rather than held
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+            const int cb = c0w + lane;
+            uint32_t pkf = pk;
+            asm volatile("" : "+v"(pkf));
+            auto chq = [&](int q) -> uint32_t {
+                return (uint32_t)c0w + ((pkf >> (8 * q)) & 63u) + (uint32_t)cs * ((pkf >> (8 * q + 6)) & 3u);
+            };
             const float2* yf = fbuf + f * G5::FB;
             // the LO row of this frame is loaded at the frame's start (loading it a frame ahead was
             // measured flat, DESIGN.md §5 k_front5); the centres of an output frame likewise
@@ -184,16 +198,15 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                 const char* ncrow = reinterpret_cast<const char*>(a.cen.ncen);
 #pragma unroll
                 for (int q = 0; q < CPT; ++q) {
-                    lov[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
-                    ncv[q] = ACC ? *reinterpret_cast<const float2*>(ncrow + (uint32_t)(cb + cs * q) * 8u)
-                                 : ysl[cb + cs * q];
+                    lov[q] = *reinterpret_cast<const float2*>(lorow + chq(q) * 8u);
+                    ncv[q] = ACC ? *reinterpret_cast<const float2*>(ncrow + chq(q) * 8u) : ysl[cb + cs * q];
                 }
             }
             [[maybe_unused]] float2 corv[CPT];
             if (f == 1) {
                 const char* corow = reinterpret_cast<const char*>(a.cen.cor);
 #pragma unroll
-                for (int q = 0; q < CPT; ++q) corv[q] = *reinterpret_cast<const float2*>(corow + (uint32_t)(cb + cs * q) * 8u);
+                for (int q = 0; q < CPT; ++q) corv[q] = *reinterpret_cast<const float2*>(corow + chq(q) * 8u);
             }
             auto zq = [&](int q) {   // z - c' of channel slot q
                 const float2 lo = lov[q];
@@ -233,19 +246,19 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                     acc[q][12] = make_float2(0.f, 0.f);
                     ph[q] = phase_atan2(y.y + corv[q].y, y.x + corv[q].x);
                     if (out) {
-                        const int c = cb + cs * q;
+                        const int sl = cb + cs * q;
                         // avgIQ only while the accumulator is armed (mkid_set_accumulator; the
                         // reference accumulates on demand, startAccumulator / avgIQ_ctrl,
                         // ROACH_Setup.py:654-659). One owner per entry: a plain read-add-write (LDS
                         // float atomics stalled every wave's LDS traffic on output frames)
                         if (ACC) {
-                            float2 ysv = ysl[c];
+                            float2 ysv = ysl[sl];
                             ysv.x += y.x;
                             ysv.y += y.y;
-                            ysl[c] = ysv;
+                            ysl[sl] = ysv;
                         }
                         if (a.iqtap) {               // uniform; the IQ-tap channel's sample by select
-                            const bool hit = c == a.iq_ch;
+                            const bool hit = (int)chq(q) == a.iq_ch;
                             const float2 yt = make_float2(y.x + a.cen.tap_off.x, y.y + a.cen.tap_off.y);
                             const uint32_t v = (uint32_t)(uint16_t)iq16(yt.x) | ((uint32_t)(uint16_t)iq16(yt.y) << 16);
                             iqv = hit ? v : iqv;
@@ -260,13 +273,18 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                     char* const rrow = reinterpret_cast<char*>(raw_run + jr * C);
 #pragma unroll
                     for (int q = 0; q < CPT; ++q) {
-                        const uint32_t c = (uint32_t)(cb + cs * q);
+                        const uint32_t c = chq(q);
                         int qv = __float2int_rn(ph[q] * 8192.0f);
                         qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
+#if defined(MKID_F5_PLAIN_STORES)   // A/B variant (tools/build_variant.sh ... -- -DMKID_F5_PLAIN_STORES)
+                        if (phase_run) *reinterpret_cast<float*>(prow + c * 4u) = ph[q];
+                        *reinterpret_cast<int16_t*>(rrow + c * 2u) = (int16_t)qv;
+#else
 #ifndef MKID_XP_STAMPS
                         if (phase_run) __builtin_nontemporal_store(ph[q], reinterpret_cast<float*>(prow + c * 4u));
 #endif
                         __builtin_nontemporal_store((int16_t)qv, reinterpret_cast<int16_t*>(rrow + c * 2u));
+#endif
                     }
                     if (iqhit) *reinterpret_cast<uint32_t*>(a.iqtap + 2 * ((k_b >> 1) + jr)) = iqv;
                 }
@@ -283,8 +301,9 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
     if (ACC)
 #pragma unroll
         for (int q = 0; q < CPT; ++q) {
-            const float2 ys = ysl[c0 + cs * q];
-            ysum_add(a.ysum, c0 + cs * q, ys.x, ys.y);
+            const float2 ys = ysl[c0w + (int)(threadIdx.x & 63) + cs * q];
+            const int c = (int)c0w + (int)((pk >> (8 * q)) & 63u) + cs * (int)((pk >> (8 * q + 6)) & 3u);
+            ysum_add(a.ysum, c, ys.x, ys.y);
         }
 }
 
@@ -449,9 +468,9 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
         // ---------------- select waves, one frame behind the transform waves --------------------
         const int sw = wave - G::FW;
         if (sw < G::SW3)
-            select_run<3, ACC, false>(a, fbuf, ysl, sw * 64 + L, 512, k_b, k_start, nrun, nit, ring, 0);
+            select_run<3, ACC, false>(a, fbuf, ysl, sw * 64, 512, k_b, k_start, nrun, nit, ring, 0);
         else
-            select_run<2, ACC, true>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64 + L, 256, k_b, k_start, nrun, nit,
+            select_run<2, ACC, true>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64, 256, k_b, k_start, nrun, nit,
                                      ring, tid - (G::FW + G::SW3) * 64);
     }
 }

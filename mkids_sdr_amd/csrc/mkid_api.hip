@@ -124,7 +124,7 @@ struct mkid_ctx {
     // bin-parity sign of K4 folded in: P is even, so the sign depends on k mod P only)
     std::vector<float2> h_lo;      // [P][C]
     std::vector<int32_t> h_bins;   // [C]
-    // select-slot order of the N = 2048 front end (k_front3): d_slot_ch[slot] = channel (slot_order
+    // select-slot order of the N = 2048 / 4096 front ends (k_front3, k_front5): d_slot_ch[slot] = channel (slot_order
     // below; MKID_SLOT_ORDER=0 keeps the identity)
     int16_t* d_slot_ch = nullptr;
     bool slot_order_on = true;
@@ -511,7 +511,7 @@ int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
     return upload_lo_folded(c);
 }
 
-// k_front3 select-slot order: plan::slot_order (mkid_plan.cpp)
+// k_front3 (N = 2048) / k_front5 select-slot order: plan::slot_order (mkid_plan.cpp)
 using plan::slot_order;
 
 static int upload_slot_order(mkid_ctx* c) {
@@ -558,15 +558,19 @@ int mkid_set_lpf(mkid_ctx* c, const int16_t* taps, int32_t n) {
 
 // Centred low-pass constants (mkid_internal.h Centring): G = sum_i g_i (exact: g_i = k_i / 2^11),
 // c' = fp32(c / G), r = fp32(G c' - c) evaluated in float64 (G c' is exact there: 16 x 24 bits), so
-// y' + r = y - c up to the rounding of r (|r| ~ 2^-24 |c|). G = 0 (all taps zero): c' = 0, r = -c.
+// y' + r = y - c up to the rounding of r (|r| ~ 2^-24 |c|). |G| < kCentringMinGain (taps with a
+// small DC gain, all-zero taps): c' = 0, r = -c, the uncentred form — c' = c / G would grow as 1 / G
+// and the low-pass accumulation's fp32 rounding with it.
+static constexpr double kCentringMinGain = 0.25;
 static int upload_centring(mkid_ctx* c) {
     double G = 0.0;
     for (int i = 0; i < kFirTaps; ++i) G += (double)c->lpf.g[i];
+    const bool centred = std::fabs(G) >= kCentringMinGain;
     std::vector<float2> nc((size_t)c->C), cr((size_t)c->C);
     c->h_gc.assign(2 * (size_t)c->C, 0.0);
     for (int ch = 0; ch < c->C; ++ch) {
         const double ci = c->h_ic[ch], cq = c->h_qc[ch];
-        const float pi = G != 0.0 ? (float)(ci / G) : 0.f, pq = G != 0.0 ? (float)(cq / G) : 0.f;
+        const float pi = centred ? (float)(ci / G) : 0.f, pq = centred ? (float)(cq / G) : 0.f;
         nc[ch] = make_float2(-pi, -pq);
         cr[ch] = make_float2((float)(G * pi - ci), (float)(G * pq - cq));
         c->h_gc[2 * ch] = G * pi;
@@ -582,9 +586,10 @@ static float2 tap_offset(const mkid_ctx* c) {
     return make_float2((float)c->h_gc[2 * c->iq_ch], (float)c->h_gc[2 * c->iq_ch + 1]);
 }
 
-// the avgIQ accumulator after an armed call of J rows: the device summed y', the host adds J G c'
+// the avgIQ accumulator after an armed call of J rows: the device summed y', the host adds J G c'.
+// acc_rows < 0: a failed call left partial sums; the average stays invalid until re-armed.
 static void acc_account(mkid_ctx* c, int64_t J) {
-    if (!c->acc_on) return;
+    if (!c->acc_on || c->acc_rows < 0) return;
     c->acc_rows += J;
     for (size_t i = 0; i < c->acc_off.size(); ++i) c->acc_off[i] += (double)J * c->h_gc[i];
 }
@@ -764,7 +769,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.taps = c->lpf;
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
-        fa.slot_ch = c->N == 2048 ? c->d_slot_ch : nullptr;   // k_front3 at N = 2048 only
+        fa.slot_ch = (c->N == 2048 || c->N == 4096) ? c->d_slot_ch : nullptr;   // k_front3 at N = 2048, k_front5
         tstart(c, MKID_K_FRONT, &kt, A);
         HIPCHK(c, launch_fused(N, fa, A));
         tstop(c, &kt, A);
@@ -891,6 +896,7 @@ int mkid_process_device(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_ph
     const int r = c->fused ? process_fused(c, d_iq, n, d_phase, d_events, cap, d_counts)
                            : process_split(c, d_iq, n, d_phase, d_events, cap, d_counts);
     if (r == MKID_OK) acc_account(c, n / c->N);
+    else if (c->acc_on) c->acc_rows = -1;   // some front-end launches may have added to the sums
     return r;
 }
 
@@ -936,8 +942,6 @@ int mkid_process(mkid_ctx* c, const int16_t* iq, int64_t n, float* phase_out, ui
         HIPCHK(c, dalloc(&c->d_ev_ws, (size_t)evcap));
     }
     int64_t produced = 0, written = 0;
-    double ysx = 0, ysy = 0;
-    (void)ysx; (void)ysy;
     for (int64_t off = 0; off < n; off += chunk) {
         const int64_t S = std::min(chunk, n - off);
         HIPCHK(c, hipMemcpyAsync(c->d_in, iq + 2 * off, (size_t)S * 4, hipMemcpyHostToDevice, c->stream));
@@ -1018,7 +1022,7 @@ int mkid_trigger_reruns(mkid_ctx* c, int64_t* total) {
 int mkid_set_accumulator(mkid_ctx* c, int32_t enable) {
     if (!c) return MKID_E_ARG;
     if (enable != 0 && enable != 1) FAIL(c, MKID_E_ARG, "enable must be 0 or 1");
-    if (enable && !c->acc_on) {   // arming starts a new average (avgIQ_ctrl strobe + startAccumulator 1)
+    if (enable) {   // every arm starts a new average (avgIQ_ctrl strobe + startAccumulator 1)
         HIPCHK(c, hipSetDevice(c->device));
         HIPCHK(c, hipMemsetAsync(c->d_ysum, 0, (size_t)c->C * 16, c->stream));
         c->acc_rows = 0;
@@ -1030,7 +1034,9 @@ int mkid_set_accumulator(mkid_ctx* c, int32_t enable) {
 
 int mkid_avg_iq(mkid_ctx* c, float* mi, float* mq) {
     if (!c || !mi || !mq) return MKID_E_ARG;
-    if (c->acc_rows <= 0)
+    if (c->acc_rows < 0)
+        FAIL(c, MKID_E_STATE, "a process call failed while the avgIQ accumulator was armed: re-arm it");
+    if (c->acc_rows == 0)
         FAIL(c, MKID_E_STATE, "the avgIQ accumulator holds no rows: arm it (mkid_set_accumulator) before processing");
     std::vector<long long> s(2 * (size_t)c->C);
     HIPCHK(c, hipSetDevice(c->device));

@@ -1,5 +1,6 @@
 // Host-side planning (mkid_plan.h): plain C++, no HIP, built into libmkidgpu.so and, with
 // -fsanitize=address,undefined, into the CPU fuzz driver tools/plan_fuzz.cpp.
+#include <array>
 #include "mkid_plan.h"
 
 #include <algorithm>
@@ -109,65 +110,106 @@ const char* plan_call(const Workspace& ws, int C, int N, int mode, int dead, int
     return nullptr;
 }
 
-// The select threads of k_front3 (C = 1024) and k_front4 (C = 2048) read Y at entry
-// yswz(bin & 511) of each sub-FFT region (regions and frames are 0 mod 32 entries apart), so a
-// channel's LDS bank pair is that entry mod 32; a ds_read_b64 costs one LDS cycle per distinct
-// address on the busiest pair of each 32-lane half (MI355X_MICROARCH.md §LDS). Slot
-// st + (C/2) q (st = 64 w + 32 h + l) is read by lane 32 h + l of wave w in instruction q; wave w
-// owns channels 128 w .. 128 w + 127 and reads them in four groups of 32. In channel order random
-// bins cost ~3.4 cycles per group. Greedy per wave: its channels by pair-class size, each into the
-// group whose cost rises least, then whose new cost is lowest, then the emptiest: ~1.9 cycles per
-// group (tools/lds_assign.py holds the same algorithm and its model).
-// k_front4 (C = 2048) has the same read pattern but loses with the order (+0.5 % with plain stores,
-// +2.6 % with its non-temporal ones: profiles/r03/r03_h_kbench_f4_slot_order.json), so only k_front3
-// takes it; mkid_slot_order still reports the C = 2048 order for the model and tests.
+// Select-slot order (mkid_slot_order). A select thread reads, per channel and frame, the Y entry
+// `key` of its bin in each region; a ds_read_b64 costs one LDS cycle per distinct address on the
+// busiest bank pair of each 32-lane half (MI355X_MICROARCH.md §LDS), and entry e sits on pair
+// e mod 32 (regions and frames are 0 mod 32 entries apart). Each select wave's channels are
+// spread over its read groups (one per half-wave and read instruction) so that a group's 32
+// channels fall on distinct pairs where the bins allow, each wave keeping its own channels (its
+// stores and LO loads stay within the same lines). Greedy per wave: channels by pair-class size,
+// each into the group whose cost rises least, then whose new cost is lowest, then the emptiest
+// (tools/lds_assign.py holds the same algorithm and its model).
+//   k_front3, C = 1024 (N = 2048): key yswz(bin & 511); wave w owns channels 128 w .. 128 w + 127,
+//     slot st + 512 q (st = 64 w + 32 h + l) is lane 32 h + l of wave w in read instruction q:
+//     random bins ~3.4 cycles per group in channel order, ~1.9 ordered (PMC 287 M -> 156 M).
+//   k_front5, C = 2048 (N = 4096): key yswz(bin & 511) + 4 REG s (the pre-combined region P^s,
+//     s = bit 9 of the bin: same pair, another address); select wave sw < 8 owns channels
+//     64 sw + l + 512 q (q < 3, 6 groups), wave 8 + v owns 1536 + 64 v + l + 256 q (q < 2, 4 groups).
+namespace {
+void assign_groups(const std::vector<int>& yo, int ng, std::vector<std::vector<int>>& member) {
+    constexpr int GS = 32;
+    const int B = (int)yo.size();
+    int cnt[32] = {0};
+    for (int i = 0; i < B; ++i) ++cnt[yo[i] & 31];
+    std::vector<int> order(B);
+    for (int i = 0; i < B; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        const int ka = yo[a] & 31, kb = yo[b] & 31;
+        if (cnt[ka] != cnt[kb]) return cnt[ka] > cnt[kb];
+        if (ka != kb) return ka < kb;
+        return yo[a] < yo[b];
+    });
+    std::vector<int> size(ng, 0), gmax(ng, 0);
+    std::vector<std::array<int, 32>> mult(ng);
+    for (auto& m : mult) m.fill(0);
+    std::vector<std::vector<int>> seen(ng);
+    member.assign(ng, {});
+    for (int i : order) {
+        const int k = yo[i] & 31;
+        int bg = -1, bk0 = 0, bk1 = 0, bk2 = 0;
+        bool bsame = false;
+        for (int g = 0; g < ng; ++g) {
+            if (size[g] >= GS) continue;
+            const bool same = std::find(seen[g].begin(), seen[g].end(), yo[i]) != seen[g].end();
+            const int m = mult[g][k] + (same ? 0 : 1);
+            const int nm = std::max(gmax[g], m);
+            const int k0 = nm - gmax[g], k1 = nm, k2 = size[g];
+            if (bg < 0 || k0 < bk0 || (k0 == bk0 && (k1 < bk1 || (k1 == bk1 && k2 < bk2)))) {
+                bg = g; bk0 = k0; bk1 = k1; bk2 = k2; bsame = same;
+            }
+        }
+        member[bg].push_back(i);
+        ++size[bg];
+        if (!bsame) {
+            seen[bg].push_back(yo[i]);
+            ++mult[bg][k];
+        }
+        gmax[bg] = std::max(gmax[bg], mult[bg][k]);
+    }
+}
+
+int yswz_entry(int b) {
+    const int k = b & 511;
+    return k ^ ((k >> 2) & 14);
+}
+}  // namespace
+
 void slot_order(const std::vector<int32_t>& bins, int C, std::vector<int16_t>& out) {
     out.resize(C);
     for (int i = 0; i < C; ++i) out[i] = (int16_t)i;
     if ((C != 1024 && C != 2048) || (int)bins.size() < C) return;
-    constexpr int B = 128, NG = 4, GS = 32;
-    auto yoff = [](int b) { const int k = b & 511; return k ^ ((k >> 2) & 14); };
-    for (int w = 0; w < C / B; ++w) {
-        int cnt[32] = {0};
-        int yo[B];
-        for (int i = 0; i < B; ++i) {
-            yo[i] = yoff(bins[B * w + i]);
-            ++cnt[yo[i] & 31];
+    // per wave: the slots of its read groups (group j = read instruction j >> 1, half j & 1)
+    struct Wave { int base, stride, nq; };
+    std::vector<Wave> waves;
+    if (C == 1024) {
+        for (int w = 0; w < 8; ++w) waves.push_back({64 * w, 512, 2});
+    } else {
+        for (int w = 0; w < 8; ++w) waves.push_back({64 * w, 512, 3});
+        for (int v = 0; v < 4; ++v) waves.push_back({1536 + 64 * v, 256, 2});
+    }
+    constexpr int kRegion4 = 4 * 576;   // k_front5: P^1 regions start 4 REG entries after P^0
+    for (const Wave& wv : waves) {
+        const int ng = 2 * wv.nq;
+        // the wave's channels: k_front3 owns 128 consecutive channels (its slot order predates the
+        // k_front5 one and is kept bit-identical); k_front5 the natural channels of its slots
+        std::vector<int> chans;
+        if (C == 1024) {
+            const int w = wv.base / 64;
+            for (int i = 0; i < 128; ++i) chans.push_back(128 * w + i);
+        } else {
+            for (int q = 0; q < wv.nq; ++q)
+                for (int l = 0; l < 64; ++l) chans.push_back(wv.base + l + wv.stride * q);
         }
-        std::vector<int> order(B);
-        for (int i = 0; i < B; ++i) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-            const int ka = yo[a] & 31, kb = yo[b] & 31;
-            if (cnt[ka] != cnt[kb]) return cnt[ka] > cnt[kb];
-            if (ka != kb) return ka < kb;
-            return yo[a] < yo[b];
-        });
-        int size[NG] = {0}, gmax[NG] = {0}, mult[NG][32] = {{0}};
-        std::vector<int> seen[NG];
-        int member[NG][GS];
-        for (int i : order) {
-            const int k = yo[i] & 31;
-            int bg = -1, bk0 = 0, bk1 = 0, bk2 = 0;
-            bool bsame = false;
-            for (int g = 0; g < NG; ++g) {
-                if (size[g] >= GS) continue;
-                const bool same = std::find(seen[g].begin(), seen[g].end(), yo[i]) != seen[g].end();
-                const int m = mult[g][k] + (same ? 0 : 1);
-                const int nm = std::max(gmax[g], m);
-                const int k0 = nm - gmax[g], k1 = nm, k2 = size[g];
-                if (bg < 0 || k0 < bk0 || (k0 == bk0 && (k1 < bk1 || (k1 == bk1 && k2 < bk2)))) {
-                    bg = g; bk0 = k0; bk1 = k1; bk2 = k2; bsame = same;
-                }
-            }
-            member[bg][size[bg]++] = B * w + i;
-            if (!bsame) {
-                seen[bg].push_back(yo[i]);
-                ++mult[bg][k];
-            }
-            gmax[bg] = std::max(gmax[bg], mult[bg][k]);
+        std::vector<int> yo(chans.size());
+        for (size_t i = 0; i < chans.size(); ++i) {
+            const int b = bins[chans[i]];
+            yo[i] = yswz_entry(b) + (C == 2048 ? kRegion4 * ((b >> 9) & 1) : 0);
         }
-        for (int g = 0; g < NG; ++g)
-            for (int l = 0; l < GS; ++l) out[64 * w + 32 * (g & 1) + l + (C / 2) * (g >> 1)] = (int16_t)member[g][l];
+        std::vector<std::vector<int>> member;
+        assign_groups(yo, ng, member);
+        for (int g = 0; g < ng; ++g)
+            for (int l = 0; l < 32; ++l)
+                out[wv.base + 32 * (g & 1) + l + wv.stride * (g >> 1)] = (int16_t)chans[member[g][l]];
     }
 }
 

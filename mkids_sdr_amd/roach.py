@@ -15,12 +15,13 @@ Register map:
            capture_load_thresh, conv_phase_centers/conv_phase_load_centers,
            capture_Baseline_alpha, capture_base_Kf, capture_base_Kq, capture_base_thresh
   control  startDAC, DRAM_LUT_rd_valid, startAccumulator, avgIQ_ctrl, startSnap, snapPhase_ctrl,
-           ch_we, startBuffer
+           ch_we, startBuffer, conv_phase_startSnap{I,Q,IQ,Phase} / conv_phase_snap{...}_ctrl
   readback avgIQ_bram, snapPhase_bram (ROACH_Pulses.py snapshot, swapped halves), qdr0_memory
            (longsnapshot, ROACH_Pulses.py:433-551), conv_phase_snapPhase_bram /
-           conv_phase_snapIQ_bram with conv_phase_ch_we_Phase / conv_phase_ch_we_IQ
-           (pulse_triggering_v2.py:36-95, pulse_triggering_IQ.py:36-147), pulses_addr,
-           pulses_bram0/1
+           conv_phase_snapIQ_bram / conv_phase_snapI_bram / conv_phase_snapQ_bram with
+           conv_phase_ch_we_Phase / conv_phase_ch_we_IQ, one shared capture per startSnap strobe
+           (pulse_triggering_v2.py:36-95, pulse_triggering_IQ.py:36-147, ROACH_Pulses_IQ.py:357-407,
+           readouttesterIQ.py:34-88), pulses_addr, pulses_bram0/1
 Errors are raised as RuntimeError (katcp semantics, pulse_triggering_v2.py:177-179).
 """
 import re
@@ -32,6 +33,15 @@ from . import codecs, replay, lut, packets
 
 FIR_RE = re.compile(r'^FIR_b(\d+)b(\d+)$')
 PULSE_RING = 2 ** 14          # pulses_bram0/1 depth (ROACH_Pulses.py:799-800)
+# conv_phase snapshot BRAMs: bytes per phase row in the read (one '>h' sample per 32-bit word at
+# bytes [2:4] for I, Q and phase, readouttesterIQ.py:71-74; 16 bytes per 2 rows for the packed IQ
+# BRAM, pulse_triggering_IQ.py:121-147) and the startSnap strobe that arms each
+SNAP_ROW_BYTES = {'conv_phase_snapI_bram': 4, 'conv_phase_snapQ_bram': 4,
+                  'conv_phase_snapPhase_bram': 4, 'conv_phase_snapIQ_bram': 8}
+SNAP_STROBES = {'conv_phase_startSnapI': 'conv_phase_snapI_bram',
+                'conv_phase_startSnapQ': 'conv_phase_snapQ_bram',
+                'conv_phase_startSnapPhase': 'conv_phase_snapPhase_bram',
+                'conv_phase_startSnapIQ': 'conv_phase_snapIQ_bram'}
 
 
 class DeviceConfig:
@@ -84,6 +94,8 @@ class FpgaClient:
         self.resonators = []             # RESDIFF parameter dicts (set_resonators)
         self._adc_cache = None
         self.boffile = None
+        self._armed = set()              # conv_phase snapshot BRAMs armed by a startSnap strobe
+        self._snaps = {}                 # BRAM -> the capture it holds
 
     # ---- katcp surface -----------------------------------------------------------------------
     def progdev(self, boffile):
@@ -97,6 +109,7 @@ class FpgaClient:
         self._wire = packets.WireStream(self.fs, self.N)
         self.ring = packets.PulseRing()
         self._adc_cache = None
+        self._armed, self._snaps = set(), {}
         return 'ok'
 
     def is_connected(self):
@@ -140,9 +153,15 @@ class FpgaClient:
             self._buffering = bool(value & 1)
         elif name == 'conv_phase_ch_we_IQ' and self._chan is not None:
             self._chan.set_iq_tap(value)
+        elif name in SNAP_STROBES:
+            # conv_phase_startSnap{I,Q,IQ,Phase} 0 -> 1 (after the _ctrl strobe) arms that BRAM:
+            # its next read takes a new capture, shared by every BRAM armed with it
+            if rising:
+                self._armed.add(SNAP_STROBES[name])
+                self._snaps.pop(SNAP_STROBES[name], None)
         elif name in ('startAccumulator', 'startSnap', 'startDAC', 'avgIQ_ctrl', 'snapPhase_ctrl',
-                      'snapqdr_ctrl', 'ch_we', 'conv_phase_ch_we_Phase', 'conv_phase_startSnapIQ',
-                      'conv_phase_startSnapPhase', 'conv_phase_snapIQ_ctrl', 'conv_phase_snapPhase_ctrl'):
+                      'snapqdr_ctrl', 'ch_we', 'conv_phase_ch_we_Phase', 'conv_phase_snapIQ_ctrl',
+                      'conv_phase_snapPhase_ctrl', 'conv_phase_snapI_ctrl', 'conv_phase_snapQ_ctrl'):
             pass  # control strobes: state is read back through self.regs
         return None
 
@@ -185,12 +204,8 @@ class FpgaClient:
             # longsnapshot: 2 Fix16_13 samples per 32-bit word, '>h' in time order
             raw = self._raw_of(self.regs.get('ch_we', 0), size // 2)
             return raw.astype('>i2').tobytes()[:size]
-        if name == 'conv_phase_snapPhase_bram':
-            raw = self._raw_of(self.regs.get('conv_phase_ch_we_Phase', 0), size // 4)
-            return codecs.encode_conv_phase_snap(raw)[:size]
-        if name == 'conv_phase_snapIQ_bram':
-            I, Q = self._iq_of(self.regs.get('conv_phase_ch_we_IQ', 0), size // 8)
-            return codecs.encode_iq_snap(I, Q)[:size]
+        if name in SNAP_ROW_BYTES:
+            return self._read_conv_phase_snap(name, size)
         if name in ('pulses_bram0', 'pulses_bram1'):
             return self.ring.read(name, size, offset)
         if name in self.regs and isinstance(self.regs[name], bytes):
@@ -315,20 +330,51 @@ class FpgaClient:
             out.append(np.clip(np.rint(phase[:, ch] * np.float32(8192)), -25736, 25736).astype(np.int64))
         return np.concatenate(out) if out else np.zeros(0, np.int64)
 
-    def _iq_of(self, ch, npairs):
-        """Low-pass I/Q of channel ch for the next npairs phase samples (device IQ tap)."""
+    def _capture(self, rows):
+        """One snapshot capture of the next `rows` phase rows: the low-pass I/Q of the channel
+        conv_phase_ch_we_IQ selects (device IQ tap, int16 ADC-count units) and the Fix16_13 phase
+        of the channel conv_phase_ch_we_Phase selects, both from the same process calls, so the
+        k-th I/Q pair and the k-th phase sample are the same row of the stream (the firmware's
+        snap blocks share one capture trigger, readouttesterIQ.py:43-54)."""
         c = self.sync()
-        c.set_iq_tap(ch)
+        c.set_iq_tap(self.regs.get('conv_phase_ch_we_IQ', 0))
+        ph_ch = self.regs.get('conv_phase_ch_we_Phase', 0)
         step = max(1, int(c.cfg.max_chunk) // self.N)
-        out = []
-        left = npairs
+        iq, raw = [], []
+        left = rows
         while left > 0:
             n = min(step, left)
-            self._process(c, n)
-            out.append(c.iq_tap())
+            phase, _ = self._process(c, n)
+            iq.append(c.iq_tap())
+            raw.append(np.clip(np.rint(phase[:, ph_ch] * np.float32(8192)), -25736, 25736))
             left -= n
-        iq = np.concatenate(out).astype(np.int64) if out else np.zeros((0, 2), np.int64)
-        return iq[:, 0], iq[:, 1]
+        iq = np.concatenate(iq).astype(np.int64) if iq else np.zeros((0, 2), np.int64)
+        raw = np.concatenate(raw).astype(np.int64) if raw else np.zeros(0, np.int64)
+        return dict(I=iq[:, 0], Q=iq[:, 1], phase=raw)
+
+    def _read_conv_phase_snap(self, name, size):
+        """conv_phase_snap{I,Q,IQ,Phase}_bram. A BRAM armed by its startSnap strobe is filled by
+        one capture taken at the first read after the strobe, shared by every BRAM armed with it
+        and held until the next strobe (ROACH_Pulses_IQ.py:375-394 reads I then Q of one capture).
+        A BRAM that was never armed free-runs: every read is a fresh capture of its own."""
+        rows = size // SNAP_ROW_BYTES[name]
+        if name in self._armed:
+            cap = self._capture(rows)
+            for b in self._armed:
+                self._snaps[b] = cap
+            self._armed.clear()
+        elif name in self._snaps:
+            cap = self._snaps[name]
+        else:
+            cap = self._capture(rows)
+        if len(cap['phase']) < rows:
+            raise RuntimeError('Request read failed: %s holds %d samples of this capture, %d asked'
+                               % (name, len(cap['phase']), rows))
+        if name == 'conv_phase_snapIQ_bram':
+            return codecs.encode_iq_snap(cap['I'][:rows], cap['Q'][:rows])[:size]
+        key = dict(conv_phase_snapI_bram='I', conv_phase_snapQ_bram='Q',
+                   conv_phase_snapPhase_bram='phase')[name]
+        return codecs.encode_conv_phase_snap(cap[key][:rows])[:size]
 
     def _read_snap_phase(self, size):
         nsamp = size // 2
@@ -531,6 +577,24 @@ class RoachPulses:
             self.roach.write_int('startSnap', 1)
             data += self.roach.read('snapPhase_bram', 4 * L)
         return codecs.decode_snap_phase(data)
+
+    def snapshot_iq(self, ch_we=27, steps=1, L=2 ** 15):
+        """ROACH_Pulses_IQ.py:357-407 (snapshot): per step arm conv_phase_snapI/Q, read 4L bytes
+        of each BRAM, one '>h' sample per word at bytes [2:4]; phase = arctan2(Q, I) in degrees.
+        Returns (Iraw, Qraw, phase)."""
+        self.roach.write_int('conv_phase_ch_we_IQ', ch_we)
+        bin_i, bin_q = b'', b''
+        for _ in range(steps):
+            for name, v in (('conv_phase_startSnapI', 0), ('conv_phase_startSnapQ', 0),
+                            ('conv_phase_snapI_ctrl', 1), ('conv_phase_snapQ_ctrl', 1),
+                            ('conv_phase_snapI_ctrl', 0), ('conv_phase_snapQ_ctrl', 0),
+                            ('conv_phase_startSnapI', 1), ('conv_phase_startSnapQ', 1)):
+                self.roach.write_int(name, v)
+            bin_i += self.roach.read('conv_phase_snapI_bram', 4 * L)
+            bin_q += self.roach.read('conv_phase_snapQ_bram', 4 * L)
+        Iraw = codecs.decode_conv_phase_snap(bin_i)
+        Qraw = codecs.decode_conv_phase_snap(bin_q)
+        return Iraw, Qraw, 360 * np.arctan2(Qraw, Iraw) / (2 * np.pi)
 
     def loadSingleThreshold(self, ch, nsigma=2.5):
         phase = self.snapshot_raw(ch)

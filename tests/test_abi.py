@@ -54,12 +54,13 @@ def test_host_only_entry_points():
 
 @pytest.mark.parametrize('C', [1024, 2048])
 def test_slot_order_host(C):
-    """The select-slot order of k_front3 / k_front4 (mkid_slot_order): a permutation that keeps
+    """The select-slot order of k_front3 / k_front5 (mkid_slot_order): a permutation that keeps
     each wave's 128 channels, matches tools/lds_assign.py's model, and cuts the modelled Y-gather
     LDS cycles (one per distinct address on the busiest bank pair of each 32-lane half) by >= 35 %."""
     import numpy as np
     from mkids_sdr_amd import _lib
-    from tools.lds_assign import group_cost, natural_groups, slot_order_blocks, yswz
+    from tools.lds_assign import (f5_groups, f5_key, f5_waves, group_cost, natural_groups,
+                                  slot_order_blocks, slot_order_f5_waves, yswz)
     L = _lib.load()
     rng = np.random.default_rng(11)
     for trial in range(2):
@@ -69,10 +70,19 @@ def test_slot_order_host(C):
         o = out.astype(np.int64)
         assert np.array_equal(np.sort(o), np.arange(C))
         slots = np.arange(C)
-        assert np.array_equal(o // 128, (slots % (C // 2)) // 64)      # wave w keeps channels 128 w ..
-        assert np.array_equal(o, slot_order_blocks(bins, C=C))
-        yo = np.array([yswz(int(b) & 511) for b in bins])
-        nat, opt = group_cost(natural_groups(C), yo), group_cost(natural_groups(C), yo[o])
+        if C == 1024:   # k_front3: wave w keeps channels 128 w ..
+            assert np.array_equal(o // 128, (slots % (C // 2)) // 64)
+            assert np.array_equal(o, slot_order_blocks(bins, C=C))
+            yo = np.array([yswz(int(b) & 511) for b in bins])
+            nat, opt = group_cost(natural_groups(C), yo), group_cost(natural_groups(C), yo[o])
+        else:           # k_front5: each select wave keeps the natural channels of its slots, and
+            # every channel is base + l + stride q (the kernel's packed 8-bit (q, l) code)
+            for base, stride, nq in f5_waves():
+                own = np.array([base + l + stride * q for q in range(nq) for l in range(64)])
+                assert np.array_equal(np.sort(o[own]), np.sort(own))
+            assert np.array_equal(o, slot_order_f5_waves(bins))
+            key = f5_key(bins)
+            nat, opt = group_cost(f5_groups(), key), group_cost(f5_groups(), key[o])
         assert opt <= 0.65 * nat, (nat, opt)
     ident = np.zeros(256, np.int16)
     assert L.mkid_slot_order(np.arange(256, dtype=np.int32).ctypes.data_as(ctypes.c_void_p), 256,

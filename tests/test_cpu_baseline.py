@@ -62,6 +62,9 @@ def test_cpu_leg_witness_green(tmp_path, mode):
     p = out['parity']
     assert p['green'] is True, p
     assert p['phase_max_err_rad'] < 1e-6 and p['raw_flip_rate'] == 0.0
+    assert p['iq_floor_rel'] == 0.01 and p['settled_max_err_above_floor'] < 1e-6
+    assert p['settled_tone_samples_below_floor_frac'] <= 0.01
+    assert 0 <= p['channels_mostly_below_floor'] <= p['channels_below_floor'] <= 64
     assert p['packets_device'] == p['packets_oracle_chain'] == npk > 0
     assert out['one_core']['value'] > 0 and out['all_cores']['cores'] == 2
     # the mode reached the oracle trigger: the one-core leg counted the witness' packets
@@ -82,4 +85,4 @@ def test_cpu_leg_witness_red(tmp_path, perturb):
     else:
         assert p['phase_max_err_all_rows_rad'] > 5e-2 and p['phase_max_err_settled_rad'] < 1e-6
         assert p['phase_max_err_rad'] < 1e-6 and p['samples_below_floor'] > 0
-        assert p['iq_err_below_floor_max_rel'] > 2e-7
+        assert p['iq_err_below_floor_max_rel'] > p['iq_tol_rel'] == 1e-7

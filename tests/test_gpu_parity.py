@@ -18,10 +18,10 @@ pytestmark = pytest.mark.gpu
 
 PHASE_TOL = 1e-5
 # absolute IQ error bar below the IQ floor, relative to the feedline's strongest tone |y| (the
-# comb's full-scale level). Measured (round 5): the device's y - c differs from the
-# float64 oracle's by <= 5e-8 |y|max on weak channels (the FFT's comb-level rounding), so the floor
-# F = 0.02 |y|max leaves a 4x margin.
-IQ_TOL_REL = 2e-7
+# comb's full-scale level). Measured (rounds 5-6): the device's y - c differs from the
+# float64 oracle's by <= 5e-8 |y|max on weak channels (the FFT's comb-level rounding), so the bar
+# leaves a 2x margin and puts the floor at F = IQ_TOL_REL / PHASE_TOL |y|max = 0.01 |y|max.
+IQ_TOL_REL = 1e-7
 # rows after a reset until every tap of the chain sees stream samples: frame k is complete from
 # k = 2T - 1 = 7, output row j reads frames 2j + 1 - 25 .. 2j + 1, so j >= 16 (reporting only)
 SETTLE_ROWS = 16
@@ -57,22 +57,26 @@ def split_by_channel(ev):
     return out
 
 
-def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32, front='auto'):
+def run_gpu(case, thr, splits, mode=1, max_chunk=None, dead=32, front='auto', acc=True):
+    """acc: arm the avgIQ accumulator (the front ends' accumulating variants: k_front5<true>, the
+    y-sum stores of k_front / k_front3) and return its means; False runs the streaming variants
+    bench.py times and returns None for the means."""
     from mkids_sdr_amd.channelizer import Channelizer
     S = case.iq.shape[0]
     ch = Channelizer(case.C, max_chunk=max_chunk or S, dead_time=dead, front=front)
     try:
         configure(ch, case, thr, mode)
-        ch.set_accumulator(True)
+        if acc:
+            ch.set_accumulator(True)
         phases, evs = [], []
         for a, b in zip(splits[:-1], splits[1:]):
             ph, ev = ch.process(case.iq[a:b])
             phases.append(ph)
             evs.append(ev)
-        mi, mq = ch.avg_iq()
+        means = ch.avg_iq() if acc else None
     finally:
         ch.close()
-    return np.concatenate(phases), np.concatenate(evs), (mi, mq)
+    return np.concatenate(phases), np.concatenate(evs), means
 
 
 _CASES, _ORACLE = {}, {}
@@ -100,13 +104,13 @@ def oracle_of(case):
 
 
 def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=True, front='auto',
-            phase_tol=None, report=None):
+            phase_tol=None, report=None, acc=True):
     """phase_tol: per-channel phase bar [C] (default PHASE_TOL everywhere); report: a dict that
     receives the per-channel max phase error ('err') and Fix16_13 flip counts ('flips')."""
     r = oracle_of(case)
     tr = otrig.Trigger(case.C, case.fir12, thr, mode=mode, dead=dead)
     ev_o, n_o, _ = tr.run(r['raw'])
-    ph_g, ev_g, _ = run_gpu(case, thr, splits, mode, max_chunk, dead, front)
+    ph_g, ev_g, _ = run_gpu(case, thr, splits, mode, max_chunk, dead, front, acc)
 
     assert ph_g.shape == r['phase'].shape
     tones = slice(0, case.n_tones)
@@ -172,14 +176,17 @@ def compare(case, thr, splits, mode=1, max_chunk=None, dead=32, expect_events=Tr
     (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'split'),
     (2048, 2 ** 20, [0, 3 * 2 ** 17 + 4096, 2 ** 20], 6, 'auto'),   # config 5 geometry (k_front5)
     (2048, 2 ** 20, None, 6, 'split'),
+    (1024, 2 ** 20, [0, 2 ** 19, 2 ** 20], 5, 'auto-noacc'),   # the streaming variants bench times
+    (2048, 2 ** 20, [0, 3 * 2 ** 17 + 4096, 2 ** 20], 6, 'auto-noacc'),
 ])
 def test_chain_parity(gpu, C, S, splits, seed, front):
     """Full chain vs the oracle. 'auto' runs the fused front end (k_front3 for N = 512 / 1024 / 2048,
     k_front5 for N = 4096, k_front for N = 128); 'split' runs k_channelize + k_lpf_phase with z staged
-    in HBM. (Round 5 retired k_front2 and k_front4; their MKID_FRONT_V3=0 / MKID_FRONT_V5=0 cases
-    run through these default paths.)"""
+    in HBM; 'auto-noacc' runs the fused front end with the avgIQ accumulator off (k_front5<false>,
+    no y-sum stores), the variant every streaming call and bench.py run."""
     case, thr = cached_case(C, S, seed, max(1.0, S / (2 * C) / 400))
-    compare(case, thr, splits or [0, S], front=front)
+    acc = not front.endswith('-noacc')
+    compare(case, thr, splits or [0, S], front=front.replace('-noacc', ''), acc=acc)
 
 
 @pytest.mark.parametrize('mode', [0, 1, 2])

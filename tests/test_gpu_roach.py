@@ -93,6 +93,92 @@ def test_snapshot_registers_readback(gpu):
     assert len(vals) == 2048 and np.abs(np.median(vals)) < 1000
 
 
+def _iq_tone_client(C=256, seed=7):
+    """A loop-back feedline with four tones, LUTs defined and the DAC on; no rotation and no
+    centres, so arctan2(Q, I) of the low-pass output is the phase the device computes."""
+    roach = FpgaClient(n_channels=C, noise_sigma=40.0, seed=seed)
+    roach.progdev('pulse_trigger_2022_Jan_24_1322.bof')
+    freqs = list(4.0e9 + np.array([-120, -40, 30, 95]) * 1e6 + 15625.0)
+    rs = RoachSetup(roach, freqs, 4.0e9, n_channels=C)
+    rs.define_LUTs()
+    rs.toggleDAC()
+    return roach
+
+
+def _readouttester(roach, ch_we, ch_we_phase, steps, L):
+    """readouttesterIQ.py:34-83 through the shim: arm I, Q and phase together, read 4L bytes of
+    each BRAM per step, one '>h' per word at bytes [2:4]; phase_cpu = arctan2(Qraw, Iraw),
+    phase_fpga = phaseraw * 360 / 2^16 * 4 / pi (both returned in radians here)."""
+    import struct
+    roach.write_int('conv_phase_ch_we_IQ', ch_we)
+    roach.write_int('conv_phase_ch_we_Phase', ch_we_phase)
+    bin_i, bin_q, bin_p = b'', b'', b''
+    for _ in range(steps):
+        for name, v in (('conv_phase_startSnapI', 0), ('conv_phase_startSnapQ', 0),
+                        ('conv_phase_startSnapPhase', 0), ('conv_phase_snapI_ctrl', 1),
+                        ('conv_phase_snapQ_ctrl', 1), ('conv_phase_snapPhase_ctrl', 1),
+                        ('conv_phase_snapI_ctrl', 0), ('conv_phase_snapQ_ctrl', 0),
+                        ('conv_phase_snapPhase_ctrl', 0), ('conv_phase_startSnapI', 1),
+                        ('conv_phase_startSnapQ', 1), ('conv_phase_startSnapPhase', 1)):
+            roach.write_int(name, v)
+        bin_i += roach.read('conv_phase_snapI_bram', 4 * L)
+        bin_q += roach.read('conv_phase_snapQ_bram', 4 * L)
+        bin_p += roach.read('conv_phase_snapPhase_bram', 4 * L)
+    n = steps * L
+    Iraw = np.array([struct.unpack('>h', bin_i[4 * m + 2:4 * m + 4])[0] for m in range(n)])
+    Qraw = np.array([struct.unpack('>h', bin_q[4 * m + 2:4 * m + 4])[0] for m in range(n)])
+    praw = np.array([struct.unpack('>h', bin_p[4 * m + 2:4 * m + 4])[0] for m in range(n)])
+    phase_cpu = 360 * np.arctan2(Qraw, Iraw) / (2 * np.pi)
+    phase_fpga = praw * 360. / 2 ** 16 * 4 / np.pi
+    return Iraw, Qraw, praw, np.deg2rad(phase_cpu), np.deg2rad(phase_fpga)
+
+
+@pytest.mark.parametrize('steps,L', [(15, 16), (1, 2 ** 15)])
+def test_readouttester_iq_vs_phase(gpu, steps, L):
+    """The reference's CPU-vs-firmware parity probe (readouttesterIQ.py:34-88) run
+    unmodified in shape through FpgaClient: the I/Q snapshot and the phase snapshot of the same
+    channel come from one capture, and the host's arctan2(Qraw, Iraw) equals the device's
+    Fix16_13 phase within half an LSB (the device's rounding of its own float phase) + 1e-5 rad
+    (the phase bar) + the int16 rounding of the I/Q snapshot (|dphi| <= 0.5 sqrt2 / |IQ|).
+    (15, 16) is the script's own capture; (1, 2^15) is ROACH_Pulses_IQ.snapshot's depth."""
+    roach = _iq_tone_client()
+    ch = 1
+    Iraw, Qraw, praw, cpu, fpga = _readouttester(roach, ch, ch, steps, L)
+    mag = np.hypot(Iraw, Qraw)
+    assert len(Iraw) == steps * L and mag.min() > 50           # a live tone in every row
+    bar = 0.5 / 8192 + 1e-5 + 0.5 * np.sqrt(2) / (mag - 1)
+    d = np.abs(np.angle(np.exp(1j * (cpu - fpga))))
+    assert np.all(d <= bar), 'max %.3g rad over the bar (row %d)' % ((d - bar).max(), np.argmax(d - bar))
+    # the probe has power: the noise moves the phase between rows by more than the bar, so a
+    # phase snapshot from other rows than the I/Q (off by one) would fail it
+    shifted = np.abs(np.angle(np.exp(1j * (cpu[1:] - fpga[:-1]))))
+    print('rows off by one over the bar: %.3f' % (shifted > bar[1:]).mean())
+    assert (shifted > bar[1:]).any()
+    # the phase BRAM's channel selects independently (readouttesterIQ.py:29-30 uses 27 / 43)
+    Iraw2, Qraw2, praw2, cpu2, fpga2 = _readouttester(roach, ch, 2, 1, 64)
+    assert np.abs(np.angle(np.exp(1j * (cpu2 - fpga2)))).max() > 0.1
+
+
+def test_roach_pulses_iq_snapshot(gpu):
+    """ROACH_Pulses_IQ.snapshot (:357-407) through RoachPulses.snapshot_iq at L = 2^15: I and Q
+    come from one capture (held by the BRAMs until the next strobe: a second Q read without a
+    strobe returns the same words), on the tone's loop."""
+    roach = _iq_tone_client(seed=8)
+    rp = RoachPulses(roach, 4, np.loadtxt(os.path.join(GOLD, 'fir', 'matched_30us.txt')), n_channels=256)
+    I, Q, phase = rp.snapshot_iq(ch_we=2, steps=1, L=2 ** 15)
+    assert len(I) == len(Q) == len(phase) == 2 ** 15
+    mag = np.hypot(I, Q)
+    assert mag.min() > 50 and mag.std() < 0.2 * mag.mean()
+    again = codecs.decode_conv_phase_snap(roach.read('conv_phase_snapQ_bram', 4 * 2 ** 15))
+    assert np.array_equal(again, Q)
+    # the same tone's phase from the device's phase stream agrees with the snapshot's median
+    roach.write_int('conv_phase_ch_we_Phase', 2)
+    raw = codecs.decode_conv_phase_snap(roach.read('conv_phase_snapPhase_bram', 4 * 4096))
+    ph_dev = np.rad2deg(np.angle(np.exp(1j * raw / 8192.0).mean()))
+    ph_snap = np.rad2deg(np.angle(np.exp(1j * np.deg2rad(phase)).mean()))
+    assert abs((ph_dev - ph_snap + 180) % 360 - 180) < 2.0
+
+
 def test_pulse_ring_packetmaster_seconds(gpu):
     """§8(f)1 end to end: the device trigger feeds the firmware wire stream (us since PPS,
     end-of-second markers) into the pulses ring while startBuffer is 1; PulseServer ships the

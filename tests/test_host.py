@@ -103,6 +103,10 @@ def test_snapshot_codecs_match_reference_decoders():
     assert np.array_equal(setup_ref.snap_phase_decode(codecs.encode_snap_phase(raw)), raw)
     assert np.array_equal(codecs.decode_snap_phase(codecs.encode_snap_phase(raw)), raw)
     assert np.array_equal(setup_ref.conv_phase_snap_decode(codecs.encode_conv_phase_snap(raw)), raw)
+    assert np.array_equal(codecs.decode_conv_phase_snap(codecs.encode_conv_phase_snap(raw)), raw)
+    full = rng.integers(-32768, 32768, 2048)          # conv_phase_snapI/Q_bram: full int16 range
+    assert np.array_equal(setup_ref.conv_phase_snap_decode(codecs.encode_conv_phase_snap(full)), full)
+    assert np.array_equal(codecs.decode_conv_phase_snap(codecs.encode_conv_phase_snap(full)), full)
     I = rng.integers(-32768, 32768, 512)
     Q = rng.integers(-32768, 32768, 512)
     buf = codecs.encode_iq_snap(I, Q)
@@ -110,6 +114,53 @@ def test_snapshot_codecs_match_reference_decoders():
     assert np.array_equal(a, I) and np.array_equal(b, Q)
     a, b = codecs.decode_iq_snap(buf)
     assert np.array_equal(a, I) and np.array_equal(b, Q)
+
+
+def test_conv_phase_snapshot_arming():
+    """FpgaClient's conv_phase snapshot BRAMs (no GPU: the capture is stubbed with a counter).
+    The BRAMs armed by one startSnap strobe share one capture, taken at the first read after the
+    strobe; a second read without a new strobe returns the held capture; a never-armed BRAM
+    free-runs (a fresh capture per read)."""
+    from mkids_sdr_amd.roach import FpgaClient
+    roach = FpgaClient(n_channels=64, gpu=False)
+    calls = []
+
+    def fake_capture(rows):
+        k = len(calls)
+        calls.append(rows)
+        base = np.arange(rows, dtype=np.int64) + 1000 * k
+        return dict(I=base, Q=-base, phase=base // 2)
+    roach._capture = fake_capture
+
+    def arm(*names):
+        for n in names:
+            roach.write_int('conv_phase_startSnap' + n, 0)
+        for n in names:
+            roach.write_int('conv_phase_snap%s_ctrl' % n, 1)
+            roach.write_int('conv_phase_snap%s_ctrl' % n, 0)
+        for n in names:
+            roach.write_int('conv_phase_startSnap' + n, 1)
+
+    dec = codecs.decode_conv_phase_snap
+    arm('I', 'Q', 'Phase')                                      # readouttesterIQ.py:43-54
+    i = dec(roach.read('conv_phase_snapI_bram', 4 * 16))
+    q = dec(roach.read('conv_phase_snapQ_bram', 4 * 16))
+    p = dec(roach.read('conv_phase_snapPhase_bram', 4 * 16))
+    assert calls == [16]                                        # one capture for the three
+    assert np.array_equal(i, np.arange(16)) and np.array_equal(q, -i) and np.array_equal(p, i // 2)
+    assert np.array_equal(dec(roach.read('conv_phase_snapQ_bram', 4 * 8)), -i[:8])   # held
+    assert calls == [16]
+    with pytest.raises(RuntimeError):
+        roach.read('conv_phase_snapI_bram', 4 * 32)             # deeper than the capture
+    arm('I', 'Q')                                               # ROACH_Pulses_IQ.py:376-386
+    i2 = dec(roach.read('conv_phase_snapI_bram', 4 * 16))
+    assert calls == [16, 16] and i2[0] == 1000
+    assert np.array_equal(dec(roach.read('conv_phase_snapPhase_bram', 4 * 16)), p)   # not re-armed
+    a, b = codecs.decode_iq_snap(roach.read('conv_phase_snapIQ_bram', 4 * 8))      # never armed
+    b2, _ = codecs.decode_iq_snap(roach.read('conv_phase_snapIQ_bram', 4 * 8))
+    assert calls == [16, 16, 4, 4] and a[0] == 2000 and b2[0] == 3000
+    roach.progdev('x.bof')
+    assert roach._armed == set() and roach._snaps == {}
 
 
 def test_packet_codecs():
@@ -262,13 +313,13 @@ def test_cpu_baseline_tool_runs(tmp_path):
 
 
 @pytest.mark.parametrize('N', [512, 1024, 2048, 4096])
-def test_front2_index_maps_and_lds_layouts(N):
-    """k_front2.hip / k_front4.hip (N = 4096): the in-wave FFT staging reproduces numpy's FFT, the
+def test_front_index_maps_and_lds_layouts(N):
+    """k_front3.hip / k_front5.hip (N = 4096): the in-wave FFT staging reproduces numpy's FFT, the
     decimation combine of the select is exact (fp32 Horner form within 1e-6 of max |X| at 4096),
     and every LDS access pattern is bank-conflict free on gfx950."""
     import importlib.util
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    spec = importlib.util.spec_from_file_location('front2_layouts', os.path.join(root, 'tools', 'front2_layouts.py'))
+    spec = importlib.util.spec_from_file_location('front_layouts', os.path.join(root, 'tools', 'front_layouts.py'))
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     assert m.fft_emulation() < 1e-10

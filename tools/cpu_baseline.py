@@ -22,6 +22,10 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# witness bars (tests/test_gpu_parity.py IQ_TOL_REL / PHASE_TOL): the absolute IQ bar below the floor
+# and the IQ floor |y - c| >= IQ_FLOOR |y|max above which the 1e-5 rad phase bar holds
+IQ_TOL = 1e-7
+IQ_FLOOR = 0.01          # = IQ_TOL / 1e-5
 
 
 def _single_thread_env():
@@ -144,13 +148,17 @@ def witness_compare(col, witp, cfg):
     assert dph.shape == oph.shape == draw.shape, (dph.shape, oph.shape, draw.shape)
     err = np.abs((dph.astype(np.float64) - oph + np.pi) % (2 * np.pi) - np.pi)
     # the bars of tests/test_gpu_parity.py: 1e-5 rad at every sample above the IQ floor
-    # |y - c| >= 0.02 |y|max; below it the absolute IQ bar |dphi| |y - c| <= 2e-7 |y|max
+    # |y - c| >= IQ_FLOOR |y|max; below it the absolute IQ bar |dphi| |y - c| <= IQ_TOL |y|max
     ymc = np.concatenate(col['ymc']).astype(np.float64)
     settle = 16
     ymax = float(np.max(np.median(np.stack(col['ymed']), axis=0)))   # |y|max: the strongest tone
-    held = ymc >= 0.02 * ymax
+    held = ymc >= IQ_FLOOR * ymax
     low = ~held & (err >= 1e-5)
     iq_rel = float((err * ymc)[low].max() / ymax) if low.any() and ymax > 0 else 0.0
+    # tone channels only (the others carry no tone: their |y - c| is noise)
+    tones = np.asarray(cfg['tone_mask'], bool) if 'tone_mask' in cfg else np.ones(C, bool)
+    held_t, err_t = held[:, tones], err[:, tones]
+    below_t = ~held_t[settle:]
     dr = draw.astype(np.int32) - oraw.astype(np.int32)
     flips = dr != 0
     own = _trigger(trigger, cfg).run(draw)[0]
@@ -170,8 +178,13 @@ def witness_compare(col, witp, cfg):
                phase_max_err_all_rows_rad=float(err.max()),
                phase_max_err_settled_rad=float(err[settle:].max()) if err.shape[0] > settle else None,
                phase_p999999_err_rad=float(np.quantile(err, 0.999999)),
-               phase_tol_rad=1e-5, iq_err_below_floor_max_rel=iq_rel, iq_tol_rel=2e-7,
-               iq_floor_rel=0.02, samples_below_floor=int((~held).sum()), settle_rows=settle,
+               phase_tol_rad=1e-5, iq_err_below_floor_max_rel=iq_rel, iq_tol_rel=IQ_TOL,
+               iq_floor_rel=IQ_FLOOR, samples_below_floor=int((~held).sum()), settle_rows=settle,
+               settled_max_err_above_floor=float(err_t[settle:][held_t[settle:]].max())
+               if held_t[settle:].any() else None,
+               settled_tone_samples_below_floor_frac=float(below_t.mean()) if below_t.size else 0.0,
+               channels_below_floor=int(below_t.any(axis=0).sum()),
+               channels_mostly_below_floor=int((below_t.mean(axis=0) > 0.5).sum()) if below_t.size else 0,
                raw_flip_rate=float(flips.mean()), raw_max_abs_diff=int(np.abs(dr).max()),
                channels_with_flip=len(flip_ch),
                packets_device=int(dpk.size), packets_oracle_chain=int(opk.size),
@@ -194,7 +207,7 @@ def witness_compare(col, witp, cfg):
                                 for lo, hi in ((0.0, 0.3), (0.3, 1.0), (1.0, 10.0), (10.0, np.inf))
                                 for m in [(ratio >= lo) & (ratio < hi) if np.isfinite(hi) else ratio >= lo]]
         out['by_loop_ratio'][-1]['ratio'] = [10.0, 'inf (centre at the origin)']
-    green = (out['phase_max_err_rad'] <= 1e-5 and iq_rel <= 2e-7 and out['raw_max_abs_diff'] <= 1
+    green = (out['phase_max_err_rad'] <= 1e-5 and iq_rel <= IQ_TOL and out['raw_max_abs_diff'] <= 1
              and own_equal and not unexplained)
     if 'heights' in w.files:
         sys.path.insert(0, ROOT)

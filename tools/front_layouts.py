@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Checks of k_front2.hip's index maps and LDS layouts (run by tests/test_host.py on the CPU).
+"""Checks of the fused front ends' index maps and LDS layouts (k_front3.hip at N = 512 / 1024 /
+2048, k_front5.hip at N = 4096; run by tests/test_host.py on the CPU).
 
 1. numpy emulation of one wave's 512-point FFT exactly as the kernel stages it (radix-8 over
    registers, twiddle, T1 bit swaps register<->lane bits 3-5, radix-8, twiddle, T2 through LDS
@@ -53,7 +54,8 @@ def decimation_combine(N, seed=1):
 
 
 def horner_combine_f32(N=4096, seed=2):
-    """k_front4.hip's select: X[b] = (Y_0 + t (Y_1 + t (Y_2 + t Y_3))) + t4 (Y_4 + t (... + t Y_7)),
+    """The 8-way select combine as two Horner chains (k_front5 before its round-5 radix-2
+    pre-combination): X[b] = (Y_0 + t (Y_1 + t (Y_2 + t Y_3))) + t4 (Y_4 + t (... + t Y_7)),
     t = W_N^b and t4 = W_N^{4b} (both rounded from float64), in complex64 as the device's fp32 cmac
     chains; returns the max error relative to max |X|."""
     rng = np.random.default_rng(seed)
@@ -164,14 +166,11 @@ def check_layouts(N):
     # ring writes: thread t writes samples 4t'..4t'+3 (t' = t mod M/4) of one hop (8t'..8t'+7
     # at NW = 8: one dword in each plane)
     if NW == 8:
-        # k_front4 (1024 threads): 4 samples per thread, lane t at plane 4 (t & 1) + i, index
-        # t >> 1 -> lanes 2k, 2k+1 share a bank: 2-way on the 4 refill writes per iteration (the
-        # 512-thread build's 8-sample writes are conflict-free)
-        ok['ring_write'] = max(conflict_degree(lambda L, i=i, b=b: (4 * ((b + L) & 1) + i) * Q + ((b + L) >> 1), 1, 'w32')
-                               for i in range(4) for b in range(0, M // 4, 64)) <= 2
+        # k_front5: select waves 12-15 (256 threads) refill a hop, 8 samples per thread, one
+        # dword in each plane
         ok['ring_write8'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')
                                 for j in range(8) for b in range(0, M // 8, 64))
-        ok['tap_read'] = True   # k_front4 holds the taps in VGPRs
+        ok['tap_read'] = True   # k_front5 holds the PFB taps in VGPRs
     elif NW == 4:
         ok['ring_write'] = all(conflict_free(lambda L, j=j, b=b: j * Q + b + L, 1, 'w32')
                                for j in range(4) for b in range(0, M // 4, 64))

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Static instruction budget of a kernel's main loop from hipcc -S output (make asm SRC=...):
 per function, the largest loop body (a label ... backward branch to it) split by instruction
-class. Usage: python tools/isa_count.py /tmp/k_front2.hip.s [substring of the kernel symbol]"""
+class. Usage: python tools/isa_count.py /tmp/k_front3.hip.s [substring of the kernel symbol]"""
 import re
 import sys
 from collections import Counter

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Select-wave channel assignment for k_front3 (N = 2048) that minimises LDS bank conflicts of
+"""Select-wave channel assignment for k_front3 (N = 2048) and k_front5 (N = 4096) that minimises LDS bank conflicts of
 the per-channel Y gather: a ds_read_b64 group of 32 lanes costs one LDS cycle per distinct address
 on its busiest bank pair (MI355X_MICROARCH.md §LDS; Y entry i sits on bank pair i mod 32), so the
 32 channels a group reads should fall on distinct pairs. Greedy: channels by class (pair) size,
@@ -55,8 +55,8 @@ def assign(yoff, ng=32, gs=32):
 
 def slot_order(bins, C=1024):
     """slot -> channel for the select threads: slot st + (C/2) q (st = 64 w + 32 h + l) is lane l
-    of half h of wave w, read instruction q (k_front3: C = 1024, 8 select waves; k_front4: C = 2048,
-    16 waves); group index g = (q, w, h)."""
+    of half h of wave w, read instruction q (the k_front3 layout: C = 1024, 8 select waves), with
+    the groups chosen over all channels; group index g = (q, w, h)."""
     bins = np.asarray(bins)
     yoff = np.array([yswz(int(b) & 511) for b in bins])
     ng = C // 32
@@ -111,6 +111,35 @@ def slot_order_f5(bins):
     return perm
 
 
+def f5_key(bins):
+    """k_front5's Y entry per channel (round 5 radix-2 pre-combination): yswz(bin & 511) in the
+    P^s regions, s = bit 9 of the bin, 4 REG = 2304 entries apart (same bank pair, another
+    address)."""
+    bins = np.asarray(bins, np.int64)
+    return np.array([yswz(int(b) & 511) for b in bins]) + 2304 * ((bins >> 9) & 1)
+
+
+def f5_waves():
+    """k_front5's select waves as (slot base, q stride, reads per thread): waves 4-11 three
+    channels per thread, 12-15 two."""
+    return [(64 * w, 512, 3) for w in range(8)] + [(1536 + 64 * v, 256, 2) for v in range(4)]
+
+
+def slot_order_f5_waves(bins):
+    """mkid_slot_order at C = 2048 (mkid_plan.cpp slot_order): each k_front5 select wave spreads
+    its own channels (the natural channels of its slots) over its read groups (group j: read
+    instruction j >> 1, half j & 1) with the conflict-minimising greedy on f5_key."""
+    key = f5_key(bins)
+    perm = np.empty(2048, np.int64)
+    for base, stride, nq in f5_waves():
+        ch = np.array([base + l + stride * q for q in range(nq) for l in range(64)])
+        groups = assign(key[ch], ng=2 * nq, gs=32)
+        for j, members in enumerate(groups):
+            for l, c in enumerate(members):
+                perm[base + 32 * (j & 1) + l + stride * (j >> 1)] = ch[c]
+    return perm
+
+
 def natural_groups(C=1024):
     return [[64 * w + 32 * h + l + (C // 2) * q for l in range(32)] for q in range(2) for w in range(C // 128)
             for h in range(2)]
@@ -130,5 +159,7 @@ if __name__ == '__main__':
     yoff = np.array([yswz(int(b) & 511) for b in bins])
     print('C = 2048: natural %d  assigned %d' % (group_cost(natural_groups(2048), yoff),
                                                 group_cost(natural_groups(2048), yoff[slot_order(bins, 2048)])))
-    print('k_front5: natural %d  assigned %d' % (group_cost(f5_groups(), yoff),
-                                                group_cost(f5_groups(), yoff[slot_order_f5(bins)])))
+    key = f5_key(bins)
+    print('k_front5 (P^s key): natural %d  per-wave order %d  relabel bound %d' % (
+        group_cost(f5_groups(), key), group_cost(f5_groups(), key[slot_order_f5_waves(bins)]),
+        group_cost(f5_groups(), key[slot_order_f5(bins)])))

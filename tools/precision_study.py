@@ -2,7 +2,8 @@
 """Where does the fp32 chain's phase error come from? (CPU study)
 
 Runs the float64 oracle chain (oracle/chain.py) and variants of it in which ONE stage is computed
-in float32 (numpy complex64: PFB-output conversion, FFT, DDC mix, IQ low-pass, centre + atan2), on a
+in float32 (numpy complex64: PFB-output conversion, FFT, DDC mix, IQ low-pass — uncentred 'lpf' or the
+device's centred form 'lpfc' — centre + atan2), on a
 feedline with unequal per-resonator attenuation (ROACH_Setup.py:499-502) and off-origin IQ loop
 centres (ROACH_Setup.py:595-667), and reports each variant's max phase error against the float64
 chain, binned by the channel's loop radius |y - centre| relative to the strongest tone's |y|.
@@ -64,6 +65,8 @@ class Chain32(chain.OracleChain):
         return z
 
     def lpf(self, z):
+        if 'lpfc' in self.stages:
+            return self.lpf_centred(z)
         if 'lpf' not in self.stages:
             return super().lpf(z)
         nt = len(self.g)
@@ -76,6 +79,28 @@ class Chain32(chain.OracleChain):
             y = y + g[i] * zz[start:start + 2 * J:2]
         self.zhist = zz[len(zz) - (nt - 2):].astype(np.complex128)
         return y.astype(np.complex128)
+
+    def lpf_centred(self, z):
+        """The device's centred low-pass (mkid_internal.h Centring): fp32
+        y' = sum_i g_i (z_i - c') with c' = fp32(c / G), and r = fp32(G c' - c) from float64; the
+        chain carries y = y' + r + c onward (exact in float64), so the float64 phase stage sees
+        the fp32 y' + r."""
+        nt = len(self.g)
+        G = float(self.g.sum())
+        c = self.ic.astype(np.float64) + 1j * self.qc.astype(np.float64)
+        cp = (c / G).astype(np.complex64)
+        r = (G * cp.astype(np.complex128) - c).astype(np.complex64)
+        zz = np.concatenate([self.zhist, z])
+        J = z.shape[0] // 2
+        y = np.zeros((J, self.C), np.complex64)
+        g = self.g.astype(np.float32)
+        for i in range(nt):
+            start = (nt - 2) + 1 - i
+            d = (zz[start:start + 2 * J:2].astype(np.complex64) - cp[None, :]).astype(np.complex64)
+            y = (y + g[i] * d).astype(np.complex64)
+        self.zhist = zz[len(zz) - (nt - 2):].copy()
+        yc = (y + r[None, :]).astype(np.complex64)          # the fp32 y - c the device's atan2 sees
+        return yc.astype(np.complex128) + c[None, :]
 
     def phase(self, y):
         if 'atan' not in self.stages:
@@ -108,7 +133,8 @@ def main():
     edges = [0.0, 0.01, 0.03, 0.1, 0.3, 1.01]
     out = {'channels': C, 'samples': S, 'span_db': a.span, 'ratio_min': a.ratio_min,
            'bins_q': edges, 'n_per_bin': [int(((q >= lo) & (q < hi)).sum()) for lo, hi in zip(edges, edges[1:])]}
-    for st in (('pfb',), ('fft',), ('ddc',), ('lpf',), ('atan',), ('fft', 'ddc', 'lpf', 'atan')):
+    for st in (('pfb',), ('fft',), ('ddc',), ('lpf',), ('lpfc',), ('atan',), ('fft', 'ddc', 'lpf', 'atan'),
+               ('pfb', 'fft', 'ddc', 'lpfc')):
         r = Chain32(*args, stages=st).process(case.iq)
         err = np.abs(signals.wrap(r['phase'][64:] - ref['phase'][64:])).max(axis=0)
         out['+'.join(st)] = [float(err[(q >= lo) & (q < hi)].max()) if ((q >= lo) & (q < hi)).any() else None

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Phase timing of k_front4 (N = 4096) from in-kernel s_memtime stamps (a build with
--DMKID_XP_STAMPS): lane 0 of each wave of workgroups 0-3 stamps 6 points of iterations 8..15.
+"""Phase timing of the wave-specialised front ends (k_front3 'v3', k_front5 'v5') from in-kernel
+s_memtime stamps (a build with -DMKID_XP_STAMPS): lane 0 of each wave of workgroups 0-3 stamps
+the phase boundaries of iterations 8..15.
 
-    bash tools/build_variant.sh f4_stamps -- -DMKID_XP_STAMPS
-    python tools/stamps4.py build/variants/f4_stamps.so
+    bash tools/build_variant.sh f5_stamps -- -DMKID_XP_STAMPS
+    python tools/stamps4.py build/variants/f5_stamps.so 2048 v5
 Prints mean cycles per segment over waves and iterations. Timing only: the phase output of that
 build holds the stamps.
 """
@@ -15,16 +16,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-
-SEG = [('FFT phase (PFB, 3 x radix-8, T1/T2, Y write)', 0, 1), ('barrier 1 wait', 1, 2),
-       ('LO load issue + ring refill', 2, 3), ('select + DDC + low-pass + output', 3, 4),
-       ('barrier 2 wait', 4, 5), ('loop back', 5, 'next0')]
-
-
-SEG2 = [('FFT phase (PFB, 3 x radix-8, T1/T2, Y write)', 14, 0), ('barrier 1 wait', 0, 1),
-        ('refill + select + DDC + low-pass + output', 1, 2), ('barrier 2 wait', 2, 3),
-        ('loop back', 3, 'next14')]
-
 
 SEG3 = [('transform waves: PFB + sub-FFT + ring write', 0, 1), ('transform waves: barrier wait', 1, 2),
         ('transform waves: loop back', 2, 'next0'),
@@ -106,26 +97,7 @@ def main():
         np.save(os.path.join(ROOT, 'gpurun_out', 'f5_blocks.npy'), bs)
         ch.close()
         return
-    if C == 2048:   # k_front4: 8 stamps per (wave, iteration)
-        st = phase[:4 * 16 * 8 * 8 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 8)
-        seg, top = SEG, 0
-    else:           # k_front2: 16 stamp slots per (wave, iteration), loop top in slot 14
-        st = phase[:4 * 16 * 8 * 16 * 2].view(torch.int64).cpu().numpy().reshape(4, 16, 8, 16)
-        seg, top = SEG2, 14
-    out = {}
-    tot = 0.0
-    for name, a, b in seg:
-        d = st[:, :, 1:, top] - st[:, :, :-1, a] if str(b).startswith('next') else st[:, :, :, b] - st[:, :, :, a]
-        m = float(np.mean(d))
-        tot += m
-        out[name] = dict(mean=round(m), min=int(d.min()), max=int(d.max()))
-        print('%-46s %8.0f cycles  (min %6d max %6d)' % (name, m, int(d.min()), int(d.max())))
-    it = st[:, :, 1:, top] - st[:, :, :-1, top]
-    print('%-46s %8.0f cycles  (sum of segments %.0f)' % ('iteration', float(np.mean(it)), tot))
-    out['iteration'] = round(float(np.mean(it)))
-    print(json.dumps(out))
-    ch.close()
-
+    raise SystemExit('usage: stamps4.py LIB [C] v3|v3f4|v5 (k_front3 / k_front5 stamp builds)')
 
 if __name__ == '__main__':
     main()

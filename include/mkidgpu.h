@@ -99,9 +99,11 @@ int mkid_set_pfb(mkid_ctx* ctx, const float* coeffs, int32_t n);
 int mkid_pfb_effective_taps(const float* coeffs, int32_t T, int32_t N, float* out, int32_t* shift);
 /* Host-only: the channel order the fused front ends give their select threads for a bin set:
  * out[slot] = channel. C = 1024 (k_front3, N = 2048): slot st + 512 q is read by thread st in
- * instruction q, and each select wave keeps its own 128 channels. C = 2048 (k_front5, N = 4096):
- * slot 64 sw + l + 512 q (select waves sw < 8, q < 3) or 1536 + 64 v + l + 256 q (v < 4, q < 2),
- * each wave keeping the natural channels of its slots. Within a wave the order puts each
+ * instruction q, and each select wave keeps its own 128 channels. C = 2048 (the k_front5 layout,
+ * N = 4096): slot 64 sw + l + 512 q (select waves sw < 8, q < 3) or 1536 + 64 v + l + 256 q (v < 4,
+ * q < 2), each wave keeping the natural channels of its slots; reported for tools/lds_assign.py,
+ * not applied (it cut k_front5's LDS conflict cycles 2.6x but cost 2.5-6 % in time, DESIGN.md
+ * §5.3). Within a wave the order puts each
  * half-wave's 32 Y reads on distinct LDS bank pairs where the bins allow. A permutation of 0..C-1
  * (the identity for C other than 1024 and 2048). Results do not depend on it: each channel's
  * arithmetic is unchanged. Exposed for tests and tools/lds_assign.py; MKID_SLOT_ORDER=0 at context

@@ -94,6 +94,34 @@ __device__ __forceinline__ void load_hop(const FrontArgs& a, int64_t hop, int xt
     v1 = *reinterpret_cast<const uint4*>(h + 4);
 }
 
+// Pre-combination twiddles W_1024^{e + 64 r} = w0 W_16^r (w0 = W_1024^e, e = kl + 8 la), built per
+// frame from w0 with three constants: u1 = w0 W_16, vv = w0 conj(W_16) (= (-i) w0 W_16^3) and
+// u2 = w0 W_16^2; the odd quarter turns (-i) are applied exactly by the butterfly (add_mi / sub_mi).
+// Each twiddle is within 1.1e-7 of exact (tools/front_layouts.py precombine_f32); the round-5
+// recurrence wk *= W_16 reached 3.5e-7 at r = 7, and its leak of the comb's aliased bins into the
+// weak channels set config 5's IQ error.
+struct PreTw {
+    float2 u1, vv, u2;
+};
+__device__ __forceinline__ PreTw pre_twiddles(float2 w0) {
+    // (cos(pi/8), sin(pi/8)) and (1/sqrt(2), 1/sqrt(2)) as SGPR pairs (VOP3P takes neither a
+    // literal nor a single 32-bit SGPR for its 64-bit operands); op_sel picks the half
+    float a, b, h;
+    asm volatile("s_mov_b32 %0, 0x3f6c835e\n\ts_mov_b32 %1, 0x3ec3ef15\n\ts_mov_b32 %2, 0x3f3504f3"
+                 : "=s"(a), "=s"(b), "=s"(h));
+    const uint64_t ab = tap_pair(a, b), hh = tap_pair(h, h);
+    f2v m, u1, vv, u2;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(m) : "v"(f2v_of(w0)), "s"(ab));
+    // u1 = (w0.x a + w0.y b, w0.y a - w0.x b), vv = (w0.x a - w0.y b, w0.y a + w0.x b)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+        : "=v"(u1) : "v"(f2v_of(w0)), "s"(ab), "v"(m));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+        : "=v"(vv) : "v"(f2v_of(w0)), "s"(ab), "v"(m));
+    // u2 = h (w0.x + w0.y, w0.y - w0.x)
+    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(u2) : "v"(f2v_of(rot_1mi(w0))), "s"(hh));
+    return PreTw{float2_of(u1), float2_of(vv), float2_of(u2)};
+}
+
 // hop layout: sample o at plane o % 8, plane index o / 8 stored at ring3_idx(o / 8), the paired
 // plane layout of k_front3 (plane entries 64 apart adjacent, so a lane's PFB points
 // r, r + 1 are one ds_read_b64)
@@ -107,11 +135,7 @@ __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 
 // measured and dropped (DESIGN.md §5 k_front5): T1 in registers, LO one frame ahead, one Horner
 // chain, even/odd chains, unsplit Y reads, no barrier between channels, transform-wave priority
 
-// select / DDC / low-pass / phase of the CPT channels of select slots c0 + cs q (c0 = c0w + lane),
-// frame k - 1 of iteration t. Slot -> channel is the host's bank-aware order (mkid_plan.cpp
-// slot_order, a.slot_ch; nullptr: identity): each wave keeps its own channels, c0w + l + cs q'
-// (l < 64), so a thread packs its channels as 8-bit (q', l) codes in one VGPR and rebuilds them per
-// frame; the per-channel LDS slot ysl is indexed by SLOT (lane-consecutive, conflict-free).
+// select / DDC / low-pass / phase of CPT channels c0 + cs q per thread, frame k - 1 of iteration t.
 // Registers go to the low-pass state: the centring constants (mkid_internal.h Centring) are re-read
 // per frame, -c' from the per-channel LDS slot ysl (ACC = false) or, while the avgIQ accumulator
 // is armed and ysl holds its partial sums (ACC = true), from global memory; r at output frames.
@@ -121,25 +145,22 @@ __device__ __forceinline__ void ring_put(uint32_t* hop, int xt, uint4 v0, uint4 
 // and writes the 8 samples load_hop / ring_put give it. Off the transform waves' chain: -8.8 %
 // same box (profiles/r05/r05u_kbench_c5_refill.json; waves 4-7 or 4-11 instead: -7 %).
 template <int CPT, bool ACC, bool RF>
-__device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0w, int cs,
+__device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbuf, float2* ysl, int c0, int cs,
                                            int64_t k_b, int64_t k_start, int nrun, int nit, uint32_t* ring, int xt) {
     constexpr int RS = G5::RS;
     constexpr int C = G5::C;
     float2 tb[CPT];   // W_N^{bin}
     int yoff[CPT];
-    const int c0 = c0w + (int)(threadIdx.x & 63);
-    uint32_t pk = 0;  // channel of slot q: c0w + (pk >> 8q & 63) + cs (pk >> (8q + 6) & 3)
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
-        const int c = a.slot_ch ? (int)a.slot_ch[c0 + cs * q] : c0 + cs * q;
-        pk |= (uint32_t)((((c - c0w) / cs) << 6) | ((c - c0w) & 63)) << (8 * q);
+        const int c = c0 + cs * q;
         const int32_t bin = a.bins[c];
         double sn, cn;
         sincospi(-2.0 * (double)bin / G5::N, &sn, &cn);
         tb[q] = make_float2((float)cn, (float)sn);
         // P_r^s of the bin's half s = bit 9 (regions r + 4 s, r = 0..3): see the transform waves
         yoff[q] = yswz(bin & 511) + ((bin >> 9) & 1) * 4 * G5::REG;
-        ysl[c0 + cs * q] = ACC ? make_float2(0.f, 0.f) : a.cen.ncen[c];   // the thread's own slots only
+        ysl[c] = ACC ? make_float2(0.f, 0.f) : a.cen.ncen[c];   // the thread's own channels only
     }
     uint64_t gp[13];
 #pragma unroll
@@ -178,17 +199,10 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
             const bool rf = RF && 2 * p + f + 1 < nit;
             uint4 rv0, rv1;
             if (rf) load_hop(a, hr, xt, rv0, rv1);
-            // slot base and channel codes re-defined every frame so per-channel addresses are rebuilt
-            // in the loop (a few VALU) instead of being hoisted as 64-bit pointers that crowd the
-            // low-pass state
-            int lane;   // the slot base from the lane id, recomputed here rather than held
-            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
-            const int cb = c0w + lane;
-            uint32_t pkf = pk;
-            asm volatile("" : "+v"(pkf));
-            auto chq = [&](int q) -> uint32_t {
-                return (uint32_t)c0w + ((pkf >> (8 * q)) & 63u) + (uint32_t)cs * ((pkf >> (8 * q + 6)) & 3u);
-            };
+            // channel base re-defined every frame so per-channel addresses are rebuilt in the loop
+            // (a few VALU) instead of being hoisted as 64-bit pointers that crowd the low-pass state
+            int cb = c0;
+            asm volatile("" : "+v"(cb));
             const float2* yf = fbuf + f * G5::FB;
             // the LO row of this frame is loaded at the frame's start (loading it a frame ahead was
             // measured flat, DESIGN.md §5 k_front5); the centres of an output frame likewise
@@ -198,15 +212,16 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                 const char* ncrow = reinterpret_cast<const char*>(a.cen.ncen);
 #pragma unroll
                 for (int q = 0; q < CPT; ++q) {
-                    lov[q] = *reinterpret_cast<const float2*>(lorow + chq(q) * 8u);
-                    ncv[q] = ACC ? *reinterpret_cast<const float2*>(ncrow + chq(q) * 8u) : ysl[cb + cs * q];
+                    lov[q] = *reinterpret_cast<const float2*>(lorow + (uint32_t)(cb + cs * q) * 8u);
+                    ncv[q] = ACC ? *reinterpret_cast<const float2*>(ncrow + (uint32_t)(cb + cs * q) * 8u)
+                                 : ysl[cb + cs * q];
                 }
             }
             [[maybe_unused]] float2 corv[CPT];
             if (f == 1) {
                 const char* corow = reinterpret_cast<const char*>(a.cen.cor);
 #pragma unroll
-                for (int q = 0; q < CPT; ++q) corv[q] = *reinterpret_cast<const float2*>(corow + chq(q) * 8u);
+                for (int q = 0; q < CPT; ++q) corv[q] = *reinterpret_cast<const float2*>(corow + (uint32_t)(cb + cs * q) * 8u);
             }
             auto zq = [&](int q) {   // z - c' of channel slot q
                 const float2 lo = lov[q];
@@ -246,19 +261,19 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                     acc[q][12] = make_float2(0.f, 0.f);
                     ph[q] = phase_atan2(y.y + corv[q].y, y.x + corv[q].x);
                     if (out) {
-                        const int sl = cb + cs * q;
+                        const int c = cb + cs * q;
                         // avgIQ only while the accumulator is armed (mkid_set_accumulator; the
                         // reference accumulates on demand, startAccumulator / avgIQ_ctrl,
                         // ROACH_Setup.py:654-659). One owner per entry: a plain read-add-write (LDS
                         // float atomics stalled every wave's LDS traffic on output frames)
                         if (ACC) {
-                            float2 ysv = ysl[sl];
+                            float2 ysv = ysl[c];
                             ysv.x += y.x;
                             ysv.y += y.y;
-                            ysl[sl] = ysv;
+                            ysl[c] = ysv;
                         }
                         if (a.iqtap) {               // uniform; the IQ-tap channel's sample by select
-                            const bool hit = (int)chq(q) == a.iq_ch;
+                            const bool hit = c == a.iq_ch;
                             const float2 yt = make_float2(y.x + a.cen.tap_off.x, y.y + a.cen.tap_off.y);
                             const uint32_t v = (uint32_t)(uint16_t)iq16(yt.x) | ((uint32_t)(uint16_t)iq16(yt.y) << 16);
                             iqv = hit ? v : iqv;
@@ -273,18 +288,13 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
                     char* const rrow = reinterpret_cast<char*>(raw_run + jr * C);
 #pragma unroll
                     for (int q = 0; q < CPT; ++q) {
-                        const uint32_t c = chq(q);
+                        const uint32_t c = (uint32_t)(cb + cs * q);
                         int qv = __float2int_rn(ph[q] * 8192.0f);
                         qv = qv < -25736 ? -25736 : (qv > 25736 ? 25736 : qv);
-#if defined(MKID_F5_PLAIN_STORES)   // A/B variant (tools/build_variant.sh ... -- -DMKID_F5_PLAIN_STORES)
-                        if (phase_run) *reinterpret_cast<float*>(prow + c * 4u) = ph[q];
-                        *reinterpret_cast<int16_t*>(rrow + c * 2u) = (int16_t)qv;
-#else
 #ifndef MKID_XP_STAMPS
                         if (phase_run) __builtin_nontemporal_store(ph[q], reinterpret_cast<float*>(prow + c * 4u));
 #endif
                         __builtin_nontemporal_store((int16_t)qv, reinterpret_cast<int16_t*>(rrow + c * 2u));
-#endif
                     }
                     if (iqhit) *reinterpret_cast<uint32_t*>(a.iqtap + 2 * ((k_b >> 1) + jr)) = iqv;
                 }
@@ -301,9 +311,8 @@ __device__ __forceinline__ void select_run(const FrontArgs& a, const float2* fbu
     if (ACC)
 #pragma unroll
         for (int q = 0; q < CPT; ++q) {
-            const float2 ys = ysl[c0w + (int)(threadIdx.x & 63) + cs * q];
-            const int c = (int)c0w + (int)((pk >> (8 * q)) & 63u) + cs * (int)((pk >> (8 * q + 6)) & 3u);
-            ysum_add(a.ysum, c, ys.x, ys.y);
+            const float2 ys = ysl[c0 + cs * q];
+            ysum_add(a.ysum, c0 + cs * q, ys.x, ys.y);
         }
 }
 
@@ -358,13 +367,11 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
         __syncthreads();
         // the lane's stage-1 / stage-2 twiddles W_512^{L k}, W_64^{la k} (the same every frame)
         float2 w1[7], w2[7];
-        float2 w0, w16;   // W_1024^{kl + 8 la} and W_1024^64 = W_16 (the pre-combination twiddles)
+        float2 w0;   // W_1024^{kl + 8 la} (the pre-combination twiddle of output 0)
         {
             double sn, cn;
             sincospi(-2.0 * (double)(kl + 8 * la) / 1024.0, &sn, &cn);
             w0 = make_float2((float)cn, (float)sn);
-            sincospi(-2.0 / 16.0, &sn, &cn);
-            w16 = make_float2((float)cn, (float)sn);
         }
 #pragma unroll
         for (int k = 1; k < 8; ++k) {
@@ -441,14 +448,28 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
                         //   P_rw^s[k] = Y_rw[k] + (-1)^s W_1024^k Y_{rw+4}[k],  k = 64 r + kl + 8 la
                         // (W_N^{4b} = W_1024^k (-1)^{b >> 9}), so a select reads 4 regions, not 8
                         float2* yw0 = fb + rw * G::REG + ((kl + 8 * la) ^ (la << 1));
-                        float2 wk = w0;
+                        float2 w0f = w0;   // the twiddles are rebuilt per frame, not held
+                        asm volatile("" : "+v"(w0f.x), "+v"(w0f.y));
+                        const PreTw pt = pre_twiddles(w0f);
 #pragma unroll
                         for (int r = 0; r < 8; ++r) {
+                            // W_1024^{64 r + e}: w0, u1, u2, (-i) vv, (-i) w0, (-i) u1, (-i) u2, -vv
+                            const float2 wk = (r & 3) == 0 ? w0f : ((r & 3) == 1 ? pt.u1 : ((r & 3) == 2 ? pt.u2 : pt.vv));
                             const float2 y0 = yr[r];
-                            const float2 d = cmul_pk(v[r], wk);
-                            yw0[64 * r] = make_float2(y0.x + d.x, y0.y + d.y);
-                            yw[64 * r] = make_float2(y0.x - d.x, y0.y - d.y);
-                            if (r < 7) wk = cmul_pk(wk, w16);
+                            const float2 e = cmul_pk(v[r], wk);
+                            float2 p, q;
+                            if (r < 3) {
+                                p = cadd(y0, e);
+                                q = csub(y0, e);
+                            } else if (r < 7) {          // d = (-i) e
+                                p = add_mi(y0, e);
+                                q = sub_mi(y0, e);
+                            } else {                     // d = -e
+                                p = csub(y0, e);
+                                q = cadd(y0, e);
+                            }
+                            yw0[64 * r] = p;
+                            yw[64 * r] = q;
                         }
                     }
                     STAMP5(t, 1 + s);
@@ -468,9 +489,9 @@ __global__ __launch_bounds__(G5::BT, 4) void k_front5(FrontArgs a) {
         // ---------------- select waves, one frame behind the transform waves --------------------
         const int sw = wave - G::FW;
         if (sw < G::SW3)
-            select_run<3, ACC, false>(a, fbuf, ysl, sw * 64, 512, k_b, k_start, nrun, nit, ring, 0);
+            select_run<3, ACC, false>(a, fbuf, ysl, sw * 64 + L, 512, k_b, k_start, nrun, nit, ring, 0);
         else
-            select_run<2, ACC, true>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64, 256, k_b, k_start, nrun, nit,
+            select_run<2, ACC, true>(a, fbuf, ysl, 3 * 512 + (sw - G::SW3) * 64 + L, 256, k_b, k_start, nrun, nit,
                                      ring, tid - (G::FW + G::SW3) * 64);
     }
 }

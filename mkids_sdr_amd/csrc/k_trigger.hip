@@ -381,6 +381,30 @@ __global__ __launch_bounds__(kSpecThreads) void k_mf_rows(TrigSpecArgs a, int32_
     }
 }
 
+// The splice of a re-run segment s of channel c into its packet slot: nt true packets (in the
+// channel's scratch) up to the merge detection, then the speculative packets after the ndrop the
+// speculative trajectory emitted before it. Packets both trajectories emit between the merge and
+// its detection count in nt and ndrop alike, so a late detection splices the same list.
+__device__ void splice_segment(const TrigSpecArgs& a, int c, int s, int32_t nt, int32_t ndrop, bool merged) {
+    const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
+    uint64_t* slot = a.slots + sc * a.capseg;
+    const uint64_t* scratch = a.scratch + (int64_t)c * a.capseg;
+    const int32_t cnt = a.counts[sc] < a.capseg ? a.counts[sc] : a.capseg;
+    int32_t total = nt;
+    if (merged) {
+        const int32_t keep = cnt - ndrop;
+        if (nt < ndrop) {
+            for (int32_t i = 0; i < keep; ++i) slot[nt + i] = slot[ndrop + i];
+        } else if (nt > ndrop) {
+            for (int32_t i = keep - 1; i >= 0; --i)
+                if (nt + i < a.capseg) slot[nt + i] = slot[ndrop + i];
+        }
+        total = nt + (a.counts[sc] - ndrop);
+    }
+    for (int32_t i = 0; i < nt && i < a.capseg; ++i) slot[i] = scratch[i];
+    a.counts[sc] = total;
+}
+
 // Re-run segment s of channel c from the true state T and the speculative state S0 side by side.
 // Returns true if they merged; T becomes the true state at the segment end when they did not.
 __device__ bool rerun_segment(const TrigSpecArgs& a, int c, int s, const int32_t (&tap)[kFirTaps],
@@ -418,24 +442,76 @@ __device__ bool rerun_segment(const TrigSpecArgs& a, int c, int s, const int32_t
             merged = state_eq(tru, spc, a.mode);
         }
     }
-    const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
-    uint64_t* slot = a.slots + sc * a.capseg;
-    const int32_t cnt = a.counts[sc] < a.capseg ? a.counts[sc] : a.capseg;
-    int32_t total = nt;
-    if (merged) {
-        const int32_t keep = cnt - ndrop;  // speculative packets after the merge point
-        if (nt < ndrop) {
-            for (int32_t i = 0; i < keep; ++i) slot[nt + i] = slot[ndrop + i];
-        } else if (nt > ndrop) {
-            for (int32_t i = keep - 1; i >= 0; --i)
-                if (nt + i < a.capseg) slot[nt + i] = slot[ndrop + i];
+    if (!merged) T = tru;
+    splice_segment(a, c, s, nt, ndrop, merged);
+    return merged;
+}
+
+// SVF re-run on the whole wave (k_trig_fix with the filter pre-pass, a.filt): lanes 0 and 1 step
+// the true and the speculative trajectory in lockstep (one instruction stream for both, the
+// hot-loop form trig_update_svf) over the pre-filtered rows, 64 rows per block: each lane loads
+// one row's f a block ahead and the walk broadcasts them with v_readlane. The merge is tested once
+// per block (splice_segment). Called by every lane with T uniform; on return T is uniform again
+// (the true end state when the trajectories did not merge). Round 5's single-lane walk (two
+// generic trig_step per sample plus the 26-tap filter from raw rows) took 3.2 ms for one segment
+// of 16384 rows at config 3.
+__device__ bool rerun_segment_svf(const TrigSpecArgs& a, int c, int s, const int32_t (&tap)[kFirTaps],
+                                  const TrigCfg& k, TrigState& T, const TrigState& S0, int lane) {
+    __shared__ TrigState t_sh;
+    __shared__ int32_t m_sh;
+    if (!T.binit || !S0.binit || in_holdoff(T) || in_holdoff(S0)) {   // start of stream: generic walk
+        if (lane == 0) {
+            TrigState t = T;
+            m_sh = rerun_segment(a, c, s, tap, k, t, S0) ? 1 : 0;
+            t_sh = t;
         }
-        total = nt + (a.counts[sc] - ndrop);
-    } else {
-        T = tru;
+        __syncthreads();
+        const bool merged = m_sh != 0;
+        T = t_sh;
+        __syncthreads();
+        return merged;
     }
-    for (int32_t i = 0; i < nt && i < a.capseg; ++i) slot[i] = scratch[i];
-    a.counts[sc] = total;
+    const int64_t seg0 = (int64_t)s * a.L;
+    const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
+    const FastCfg q = fast_cfg(k);
+    FastSvf st = to_fast_svf(lane == 0 ? T : S0);
+    uint64_t* scratch = a.scratch + (int64_t)c * a.capseg;
+    int32_t nt = 0, ndrop = 0;
+    bool merged = false;
+    const int16_t* fp = a.filt + c;
+    int32_t fnext = seg0 + lane < seg1 ? (int32_t)fp[(seg0 + lane) * a.C] : 0;
+    for (int64_t g = seg0; g < seg1 && !merged; g += 64) {
+        const int32_t fl = fnext;
+        const int left = (int)(seg1 - g < 64 ? seg1 - g : 64);
+        fnext = g + 64 + lane < seg1 ? (int32_t)fp[(g + 64 + lane) * a.C] : 0;   // next block in flight
+        for (int i = 0; i < left; ++i) {
+            const int32_t f = __builtin_amdgcn_readlane(fl, i);
+            EvInfo ev;
+            const bool e = trig_update_svf(st, f, q, a.kf, a.kq, ev);
+            const uint64_t b = __ballot(e);
+            if (b & 1ull) {
+                if (lane == 0 && nt < a.capseg) scratch[nt] = make_packet(c, ev, f, a.j0 + g + i);
+                ++nt;
+            }
+            ndrop += (int32_t)((b >> 1) & 1ull);
+        }
+        auto same = [&](int32_t v) { return __builtin_amdgcn_readlane(v, 0) == __builtin_amdgcn_readlane(v, 1); };
+        merged = same((int32_t)st.low) && same((int32_t)(st.low >> 32)) && same((int32_t)st.band) &&
+                 same((int32_t)(st.band >> 32)) && same(st.x) && same(st.f1) && same(st.f2);
+    }
+    if (lane == 0) splice_segment(a, c, s, nt, ndrop, merged);
+    if (!merged) {   // lane 0's trajectory, broadcast
+        FastSvf t;
+        t.low = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(st.low >> 32), 0) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int32_t)st.low, 0));
+        t.band = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(st.band >> 32), 0) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int32_t)st.band, 0));
+        t.x = __builtin_amdgcn_readlane(st.x, 0);
+        t.f1 = __builtin_amdgcn_readlane(st.f1, 0);
+        t.f2 = __builtin_amdgcn_readlane(st.f2, 0);
+        T = from_fast_svf(t);
+    }
+    __syncthreads();   // lane 0's slot and scratch writes before any later segment's re-run
     return merged;
 }
 
@@ -454,7 +530,10 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
         if (lane == 0) okbits[wd] = b;
     }
     __syncthreads();
-    if (lane != 0) return;
+    // SVF with the filter pre-pass: the whole wave runs the control below (uniform) and the
+    // re-runs use two lanes (rerun_segment_svf); otherwise lane 0 alone walks
+    const bool wave_walk = a.mode == MKID_BASE_SVF && a.filt != nullptr;
+    if (!wave_walk && lane != 0) return;
     int32_t tap[kFirTaps];
 #pragma unroll
     for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
@@ -479,9 +558,11 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
             continue;
         }
         ++reruns;
-        override_ = !rerun_segment(a, c, s, tap, k, T, a.s_spec[(int64_t)s * C + c]);
+        const TrigState S0 = a.s_spec[(int64_t)s * C + c];
+        override_ = wave_walk ? !rerun_segment_svf(a, c, s, tap, k, T, S0, lane) : !rerun_segment(a, c, s, tap, k, T, S0);
         ++s;
     }
+    if (lane != 0) return;
     a.st_out[c] = override_ ? T : a.s_end[(int64_t)(a.nseg - 1) * C + c];
     if (a.reruns) a.reruns[c] = reruns;
 }

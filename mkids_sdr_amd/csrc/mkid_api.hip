@@ -124,7 +124,7 @@ struct mkid_ctx {
     // bin-parity sign of K4 folded in: P is even, so the sign depends on k mod P only)
     std::vector<float2> h_lo;      // [P][C]
     std::vector<int32_t> h_bins;   // [C]
-    // select-slot order of the N = 2048 / 4096 front ends (k_front3, k_front5): d_slot_ch[slot] = channel (slot_order
+    // select-slot order of the N = 2048 front end (k_front3): d_slot_ch[slot] = channel (slot_order
     // below; MKID_SLOT_ORDER=0 keeps the identity)
     int16_t* d_slot_ch = nullptr;
     bool slot_order_on = true;
@@ -511,7 +511,7 @@ int mkid_set_dds(mkid_ctx* c, const int16_t* li, const int16_t* lq, int32_t P) {
     return upload_lo_folded(c);
 }
 
-// k_front3 (N = 2048) / k_front5 select-slot order: plan::slot_order (mkid_plan.cpp)
+// k_front3 select-slot order: plan::slot_order (mkid_plan.cpp)
 using plan::slot_order;
 
 static int upload_slot_order(mkid_ctx* c) {
@@ -769,7 +769,7 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         fa.taps = c->lpf;
         fa.iqtap = c->iq_ch >= 0 ? c->d_iqtap + (off / N) * 2 : nullptr;
         fa.iq_ch = c->iq_ch;
-        fa.slot_ch = (c->N == 2048 || c->N == 4096) ? c->d_slot_ch : nullptr;   // k_front3 at N = 2048, k_front5
+        fa.slot_ch = c->N == 2048 ? c->d_slot_ch : nullptr;   // k_front3 at N = 2048 only
         tstart(c, MKID_K_FRONT, &kt, A);
         HIPCHK(c, launch_fused(N, fa, A));
         tstop(c, &kt, A);

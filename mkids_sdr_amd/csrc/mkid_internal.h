@@ -107,7 +107,7 @@ struct FrontArgs {
     int16_t* iqtap;         // [K/2][2] int16 low-pass output of channel iq_ch (IQ snapshot) or nullptr
     int32_t iq_ch;
     int32_t pad;
-    const int16_t* slot_ch; // [C] k_front3 (N = 2048) / k_front5: channel of select slot (nullptr: identity)
+    const int16_t* slot_ch; // [C] k_front3 (N = 2048): channel of select slot st + 512 q (nullptr: identity)
 };
 
 struct TrigSpecArgs {

@@ -122,9 +122,13 @@ const char* plan_call(const Workspace& ws, int C, int N, int mode, int dead, int
 //   k_front3, C = 1024 (N = 2048): key yswz(bin & 511); wave w owns channels 128 w .. 128 w + 127,
 //     slot st + 512 q (st = 64 w + 32 h + l) is lane 32 h + l of wave w in read instruction q:
 //     random bins ~3.4 cycles per group in channel order, ~1.9 ordered (PMC 287 M -> 156 M).
-//   k_front5, C = 2048 (N = 4096): key yswz(bin & 511) + 4 REG s (the pre-combined region P^s,
-//     s = bit 9 of the bin: same pair, another address); select wave sw < 8 owns channels
+//   k_front5 layout, C = 2048 (N = 4096): key yswz(bin & 511) + 4 REG s (the pre-combined region
+//     P^s, s = bit 9 of the bin: same pair, another address); select wave sw < 8 owns channels
 //     64 sw + l + 512 q (q < 3, 6 groups), wave 8 + v owns 1536 + 64 v + l + 256 q (q < 2, 4 groups).
+//     Computed for the model and tests only: applied in k_front5 (round 6) it cut the PMC LDS
+//     conflict cycles 390.5 M -> 152.9 M per launch but took 2.5 % (plain stores) to 6 %
+//     (non-temporal) more time, the scattered stores and the channel decoding costing more than
+//     the conflicts, which sit off the transform waves' critical chain.
 namespace {
 void assign_groups(const std::vector<int>& yo, int ng, std::vector<std::vector<int>>& member) {
     constexpr int GS = 32;

@@ -102,6 +102,7 @@ def _iq_tone_client(C=256, seed=7):
     rs = RoachSetup(roach, freqs, 4.0e9, n_channels=C)
     rs.define_LUTs()
     rs.toggleDAC()
+    roach.run(64)        # the DAC has been on a while: the filters are past their start-up rows
     return roach
 
 

@@ -329,6 +329,8 @@ def test_front_index_maps_and_lds_layouts(N):
     if N == 4096:
         assert m.horner_combine_f32() < 1e-6
         assert m.precombine_f32() < 1e-6     # k_front5's radix-2 pre-combination (round 5)
+        dev, rec = m.pre_twiddle_errors()    # round 6: direct twiddles, not the W_16 recurrence
+        assert dev < 1.2e-7 and rec > 3e-7
 
 
 def test_resdiff_matches_reference_restatement():

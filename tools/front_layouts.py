@@ -74,25 +74,53 @@ def horner_combine_f32(N=4096, seed=2):
     return float(np.abs(X - ref).max() / np.abs(ref).max())
 
 
+def pre_twiddles(recurrence=False):
+    """[8][64] complex64: k_front5's pre-combination twiddle for output 64 r + e, e = kl + 8 la, in
+    the device's fp32 arithmetic (pre_twiddles in k_front5.hip; recurrence=True: round 5's
+    wk *= W_16)."""
+    f = np.float32
+    a, b, h = f(0.92387953251128675613), f(0.38268343236508977173), f(0.70710678118654752440)
+    e = np.arange(64)
+    w0 = np.exp(-2j * np.pi * e / 1024).astype(np.complex64)
+    out = np.empty((8, 64), np.complex64)
+    if recurrence:
+        w16 = np.complex64(np.exp(-2j * np.pi / 16))
+        wk = w0.copy()
+        for r in range(8):
+            out[r] = wk
+            wk = (wk * w16).astype(np.complex64)
+        return out
+    x, y = w0.real.astype(np.float64), w0.imag.astype(np.float64)
+    mx, my = (x * a).astype(f), (y * a).astype(f)
+    fma = lambda p, q, c: (p * np.float64(q) + np.float64(c)).astype(f)
+    u1 = fma(y, b, mx) + 1j * fma(-x, b, my)
+    vv = fma(-y, b, mx) + 1j * fma(x, b, my)
+    u2 = ((x + y).astype(f) * h).astype(f) + 1j * ((y - x).astype(f) * h).astype(f)
+    for r, t in enumerate((w0, u1, u2, -1j * vv, -1j * w0, -1j * u1, -1j * u2, -vv)):
+        out[r] = t
+    return out
+
+
+def pre_twiddle_errors():
+    """max |twiddle - exact| of the device construction and of round 5's recurrence."""
+    k = 64 * np.arange(8)[:, None] + np.arange(64)[None, :]
+    ex = np.exp(-2j * np.pi * k / 1024)
+    return (float(np.abs(pre_twiddles() - ex).max()), float(np.abs(pre_twiddles(True) - ex).max()))
+
+
 def precombine_f32(N=4096, seed=3):
-    """k_front5.hip (round 5): the transform wave that holds sub-FFTs r and r + 4 writes
-    P_r^s[k] = Y_r[k] + (-1)^s W_1024^k Y_{r+4}[k] (W_1024^k = W_1024^{kl + 8 la} W_16^{r'} built by
-    repeated multiplication, k = 64 r' + kl + 8 la), and the select evaluates
+    """k_front5.hip: the transform wave that holds sub-FFTs r and r + 4 writes
+    P_r^s[k] = Y_r[k] + (-1)^s W_1024^k Y_{r+4}[k], k = 64 r' + e (e = kl + 8 la), with the twiddle
+    W_1024^k = w0 W_16^{r'} built as k_front5's pre_twiddles (round 6): w0 = W_1024^e and
+    u1 = w0 W_16, vv = w0 conj(W_16), u2 = w0 W_16^2 from fp32 constants, the quarter turns exact
+    (round 5 stepped wk *= W_16, 3.5e-7 at r' = 7: pre_twiddle_errors); the select evaluates
     X[b] = (P_0 + t^2 P_2) + t (P_1 + t^2 P_3), t = W_N^b, s = bit 9 of b; complex64 throughout as
     the device; returns the max error relative to max |X|."""
     rng = np.random.default_rng(seed)
     u = (rng.normal(size=N) + 1j * rng.normal(size=N)) * 3e4
     Ys = [np.fft.fft(u[w::8]).astype(np.complex64) for w in range(8)]
     k = np.arange(512)
-    base = k % 64                                   # kl + 8 la
-    w0 = np.exp(-2j * np.pi * base / 1024).astype(np.complex64)
-    w16 = np.complex64(np.exp(-2j * np.pi / 16))
-    wk = w0.copy()
-    tw = np.empty(512, np.complex64)
-    for r in range(8):                              # k = 64 r + base
-        sel = (k // 64) == r
-        tw[sel] = wk[sel]
-        wk = (wk * w16).astype(np.complex64)
+    tw = pre_twiddles()[k // 64, k % 64]
     P = {}
     for r in range(4):
         d = (Ys[r + 4] * tw).astype(np.complex64)

@@ -242,10 +242,17 @@ static void fuzz_slot_order(int iters) {
         bool perm = (int)so.size() == C;
         for (int16_t v : so) perm = perm && v >= 0 && v < C && !seen[v]++;
         CHECK(perm, "slot order is not a permutation (C %d)", C);
-        if ((C == 1024 || C == 2048) && perm)
+        if (C == 1024 && perm)   // k_front3: wave w keeps channels 128 w .. 128 w + 127
             for (int slot = 0; slot < C; ++slot) {
                 const int st = slot % (C / 2), w = st / 64;
                 CHECK(so[slot] / 128 == w, "slot %d of wave %d holds channel %d", slot, w, so[slot]);
+            }
+        if (C == 2048 && perm)   // the k_front5 layout: each wave keeps the channels of its slots
+            for (int slot = 0; slot < C; ++slot) {
+                const int wave = slot < 1536 ? (slot % 512) / 64 : 8 + ((slot - 1536) % 256) / 64;
+                const int ch = so[slot];
+                const int cw = ch < 1536 ? (ch % 512) / 64 : 8 + ((ch - 1536) % 256) / 64;
+                CHECK(cw == wave, "slot %d of wave %d holds channel %d", slot, wave, ch);
             }
     }
 }

@@ -170,6 +170,45 @@ def test_failed_call_after_planning_marks_the_stream(gpu, monkeypatch):
         ch.close()
 
 
+def test_accumulator_rearm_and_failed_call(gpu, monkeypatch):
+    """every mkid_set_accumulator(1) restarts the sums (the reference strobes avgIQ_ctrl
+    before each startAccumulator 1), armed or not; a process call that fails while the accumulator
+    is armed invalidates it (its sums may hold part of that call): mkid_avg_iq then fails with
+    MKID_E_STATE until it is re-armed."""
+    from mkids_sdr_amd import _lib
+    from mkids_sdr_amd.channelizer import Channelizer
+    C, S = 64, 1 << 14
+    case = signals.make_case(C, S, seed=46, pulses_per_ch=0.0)
+    monkeypatch.setenv('MKID_FAULT_LAUNCH', '3')
+    ch = Channelizer(C, max_chunk=S)
+    monkeypatch.delenv('MKID_FAULT_LAUNCH')
+    try:
+        configure(ch, case, np.full(C, -(1 << 30)))
+        ch.set_accumulator(True)
+        ch.process(case.iq[:S // 2])               # launch 1: fine
+        a1 = ch.avg_iq()
+        ch.set_accumulator(True)                   # re-arm while armed: the sums restart
+        with pytest.raises(_lib.MkidError) as e:
+            ch.avg_iq()
+        assert e.value.code == _lib.MKID_E_STATE   # no rows since the re-arm
+        ch.process(case.iq[S // 2:])
+        a2 = ch.avg_iq()
+        assert not np.array_equal(a1[0], a2[0])    # the second half's own mean, not both halves'
+        with pytest.raises(_lib.MkidError) as e:
+            ch.process(case.iq[:S // 2])           # launch 3: the injected failure (hook = 3)
+        assert e.value.code == _lib.MKID_E_HIP
+        with pytest.raises(_lib.MkidError) as e:
+            ch.avg_iq()
+        assert e.value.code == _lib.MKID_E_STATE and 're-arm' in str(e.value)
+        ch.reset()
+        ch.set_accumulator(True)
+        ch.process(case.iq)
+        mi, mq = ch.avg_iq()
+        assert np.isfinite(mi).all() and np.isfinite(mq).all()
+    finally:
+        ch.close()
+
+
 def test_timing_mask_and_counts_written_per_call(gpu):
     """mkid_set_timing_mask with MKID_TIMING_ONLY bits times only the named kernels (bench.py's timed
     steps record events around the front end alone); d_counts is written by each call's

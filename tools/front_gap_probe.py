@@ -33,7 +33,7 @@ def main():
     args = ap.parse_args()
     import torch
     import bench
-    from mkids_sdr_amd import _lib, codecs
+    from mkids_sdr_amd import _lib, codecs, lut
     from mkids_sdr_amd.channelizer import Channelizer
 
     C, fs = 1024, 550e6
@@ -62,9 +62,20 @@ def main():
     ch = Channelizer(C, max_chunk=S, sample_rate=fs)
     ch.set_bins(np.asarray(feed['dds']['bins']))
     ch.set_dds(feed['dds']['lut_i'], feed['dds']['lut_q'])
+    ch.set_lpf(codecs.fir_quantise(np.loadtxt(os.path.join(ROOT, 'tests/golden/fir/BlackmanFilter_250kHz.txt'))))
     ch.set_fir(np.tile(mf, (C, 1)))
-    ch.set_thresholds(np.full(C, -3000, np.int32))
+    ch.set_thresholds(np.full(C, -(1 << 30), np.int32))
     ch.synth_adc(x, S, 0, base, d_tones, d_pul, len(ps), 0.1 * N, 65.0 * N, 390 * N, 0.01 * 32767 / np.sqrt(2.0), 42)
+    # rotate the loops as tools/kbench.py does (avgIQ -> DDS phase), so the phase sits near 0 and the
+    # trigger sees the bench's packet rate
+    ch.set_accumulator(True)
+    ch.process_device(x, S, phase, d_ev, cap, d_cnt)
+    torch.cuda.synchronize()
+    mi, mq = ch.avg_iq()
+    ch.set_accumulator(False)
+    dds = lut.define_dds_lut(list(feed['f_rf']), feed['f_base'], C, fs, phase=np.arctan2(mq, mi))
+    ch.set_dds(dds['lut_i'], dds['lut_q'])
+    ch.set_thresholds(np.full(C, -3000, np.int32))
     torch.cuda.synchronize()
     stream = torch.cuda.Stream(dev)          # the context and the spin kernel share it
     ch.set_stream(stream.cuda_stream)

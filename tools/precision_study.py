@@ -112,14 +112,63 @@ class Chain32(chain.OracleChain):
         return ph, raw
 
 
+def combine_study(seeds=3, span=20.0):
+    """k_front5's decimated combine (N = 4096, 8 sub-FFTs of 512, radix-2 pre-combination in the
+    transform waves, 4-way Horner select) in complex64 on a 2048-tone comb spread over `span` dB:
+    the error at the tone bins relative to the strongest tone, for the pre-combination twiddles of
+    round 5 (wk *= W_16), of round 6 (tools/front_layouts.pre_twiddles), and directly rounded ones,
+    beside a plain fp32 4096-point FFT. The sub-FFT outputs carry the comb's 8 aliased bins, so a
+    twiddle error leaks the strong tones into the weak channels' bins."""
+    sys.path.insert(0, os.path.join(ROOT, 'tools'))
+    import front_layouts as fl
+    N, C = 4096, 2048
+    k = np.arange(512)
+    tws = {'round5_recurrence': fl.pre_twiddles(True)[k // 64, k % 64],
+           'round6_device': fl.pre_twiddles()[k // 64, k % 64],
+           'direct_rounded': np.exp(-2j * np.pi * k / 1024).astype(np.complex64)}
+    out = {name: [] for name in list(tws) + ['numpy_fp32_fft4096']}
+    for seed in range(seeds):
+        rng = np.random.default_rng(seed)
+        bins = rng.permutation(np.arange(1, N))[:C]
+        amp = 10 ** (-rng.uniform(0, span, C) / 20)
+        n = np.arange(N)
+        x = (amp[None, :] * np.exp(2j * np.pi * (np.outer(n, bins) / N + rng.uniform(size=C)[None, :]))).sum(1)
+        u = x * 3e4 / np.abs(x).max()
+        ref = np.fft.fft(u)
+        ymax = np.abs(ref[bins]).max()
+        Ys = [np.fft.fft(u[w::8].astype(np.complex64)).astype(np.complex64) for w in range(8)]
+        b = np.arange(N)
+        s_, kk = (b >> 9) & 1, b % 512
+        t = np.exp(-2j * np.pi * b / N).astype(np.complex64)
+        t2 = (t * t).astype(np.complex64)
+        for name, tw in tws.items():
+            P = {}
+            for r in range(4):
+                d = (Ys[r + 4] * tw).astype(np.complex64)
+                P[(r, 0)] = (Ys[r] + d).astype(np.complex64)
+                P[(r, 1)] = (Ys[r] - d).astype(np.complex64)
+            g = lambda r: np.where(s_ == 0, P[(r, 0)][kk], P[(r, 1)][kk])
+            X = ((g(0) + t2 * g(2)).astype(np.complex64) + t * (g(1) + t2 * g(3)).astype(np.complex64)).astype(np.complex64)
+            e = np.abs(X[bins] - ref[bins]) / ymax
+            out[name].append((float(e.max()), float(np.sqrt((e ** 2).mean()))))
+        e = np.abs(np.fft.fft(u.astype(np.complex64)).astype(np.complex64)[bins] - ref[bins]) / ymax
+        out['numpy_fp32_fft4096'].append((float(e.max()), float(np.sqrt((e ** 2).mean()))))
+    return {name: dict(max_rel_to_strongest=max(a for a, _ in v), rms_rel_to_strongest=float(np.mean([b for _, b in v])))
+            for name, v in out.items()}
+
+
 def main():
     p = argparse.ArgumentParser()
+    p.add_argument('--combine', action='store_true', help="k_front5's combine study only (combine_study)")
     p.add_argument('--channels', type=int, default=1024)
     p.add_argument('--log2', type=int, default=18)
     p.add_argument('--span', type=float, default=20.0, help='attenuation span (dB)')
     p.add_argument('--ratio-min', type=float, default=0.1, help='smallest loop radius / |centre|')
     p.add_argument('--seed', type=int, default=7)
     a = p.parse_args()
+    if a.combine:
+        print(json.dumps(dict(span_db=a.span, tones=2048, N=4096, combine=combine_study(span=a.span)), indent=1))
+        return
     C, S = a.channels, 1 << a.log2
     rng = np.random.default_rng(a.seed)
     att = rng.uniform(0.0, a.span, C)

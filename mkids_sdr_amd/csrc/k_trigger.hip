@@ -385,10 +385,10 @@ __global__ __launch_bounds__(kSpecThreads) void k_mf_rows(TrigSpecArgs a, int32_
 // channel's scratch) up to the merge detection, then the speculative packets after the ndrop the
 // speculative trajectory emitted before it. Packets both trajectories emit between the merge and
 // its detection count in nt and ndrop alike, so a late detection splices the same list.
-__device__ void splice_segment(const TrigSpecArgs& a, int c, int s, int32_t nt, int32_t ndrop, bool merged) {
+__device__ void splice_segment(const TrigSpecArgs& a, int c, int s, int32_t nt, int32_t ndrop, bool merged,
+                               const uint64_t* scratch) {
     const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
     uint64_t* slot = a.slots + sc * a.capseg;
-    const uint64_t* scratch = a.scratch + (int64_t)c * a.capseg;
     const int32_t cnt = a.counts[sc] < a.capseg ? a.counts[sc] : a.capseg;
     int32_t total = nt;
     if (merged) {
@@ -443,18 +443,65 @@ __device__ bool rerun_segment(const TrigSpecArgs& a, int c, int s, const int32_t
         }
     }
     if (!merged) T = tru;
-    splice_segment(a, c, s, nt, ndrop, merged);
+    splice_segment(a, c, s, nt, ndrop, merged, scratch);
     return merged;
 }
 
-// SVF re-run on the whole wave (k_trig_fix with the filter pre-pass, a.filt): lanes 0 and 1 step
-// the true and the speculative trajectory in lockstep (one instruction stream for both, the
-// hot-loop form trig_update_svf) over the pre-filtered rows, 64 rows per block: each lane loads
-// one row's f a block ahead and the walk broadcasts them with v_readlane. The merge is tested once
-// per block (splice_segment). Called by every lane with T uniform; on return T is uniform again
-// (the true end state when the trajectories did not merge). Round 5's single-lane walk (two
-// generic trig_step per sample plus the 26-tap filter from raw rows) took 3.2 ms for one segment
-// of 16384 rows at config 3.
+// SVF re-run of segment s of channel c on one wave (the filter pre-pass, a.filt): lanes 0 and 1
+// step the true (from T) and the speculative (from S0) trajectory in lockstep (one instruction
+// stream for both, the hot-loop form trig_update_svf) over the pre-filtered rows, 64 rows per
+// block: each lane loads one row's f a block ahead and the walk broadcasts them with v_readlane.
+// The merge is tested once per block (splice_segment). Lane 0 writes the true packets to out;
+// nt / ndrop / merged are uniform, Tend (the true end state when not merged) is uniform.
+// Round 5's single-lane walk (two generic trig_step per sample plus the 26-tap filter from raw
+// rows) took 3.2 ms for one segment of 16384 rows at config 3; this one 0.71 ms.
+__device__ bool svf_walk(const TrigSpecArgs& a, int c, int s, const TrigCfg& k, const TrigState& T,
+                         const TrigState& S0, int lane, uint64_t* out, int32_t& nt, int32_t& ndrop, TrigState& Tend) {
+    const int64_t seg0 = (int64_t)s * a.L;
+    const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
+    const FastCfg q = fast_cfg(k);
+    FastSvf st = to_fast_svf(lane == 0 ? T : S0);
+    nt = 0;
+    ndrop = 0;
+    bool merged = false;
+    const int16_t* fp = a.filt + c;
+    int32_t fnext = seg0 + lane < seg1 ? (int32_t)fp[(seg0 + lane) * a.C] : 0;
+    for (int64_t g = seg0; g < seg1 && !merged; g += 64) {
+        const int32_t fl = fnext;
+        const int left = (int)(seg1 - g < 64 ? seg1 - g : 64);
+        fnext = g + 64 + lane < seg1 ? (int32_t)fp[(g + 64 + lane) * a.C] : 0;   // next block in flight
+        for (int i = 0; i < left; ++i) {
+            const int32_t f = __builtin_amdgcn_readlane(fl, i);
+            EvInfo ev;
+            const bool e = trig_update_svf(st, f, q, a.kf, a.kq, ev);
+            const uint64_t b = __ballot(e);
+            if (b & 1ull) {
+                if (lane == 0 && nt < a.capseg) out[nt] = make_packet(c, ev, f, a.j0 + g + i);
+                ++nt;
+            }
+            ndrop += (int32_t)((b >> 1) & 1ull);
+        }
+        auto same = [&](int32_t v) { return __builtin_amdgcn_readlane(v, 0) == __builtin_amdgcn_readlane(v, 1); };
+        merged = same((int32_t)st.low) && same((int32_t)(st.low >> 32)) && same((int32_t)st.band) &&
+                 same((int32_t)(st.band >> 32)) && same(st.x) && same(st.f1) && same(st.f2);
+    }
+    if (!merged) {   // lane 0's trajectory, broadcast
+        FastSvf t;
+        t.low = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(st.low >> 32), 0) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int32_t)st.low, 0));
+        t.band = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(st.band >> 32), 0) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int32_t)st.band, 0));
+        t.x = __builtin_amdgcn_readlane(st.x, 0);
+        t.f1 = __builtin_amdgcn_readlane(st.f1, 0);
+        t.f2 = __builtin_amdgcn_readlane(st.f2, 0);
+        Tend = from_fast_svf(t);
+    }
+    return merged;
+}
+
+// The two-lane walk usable from any state: a start-of-stream state (hold-off, no baseline) takes
+// the generic single-lane walk instead (rerun_segment). Called by every lane with T uniform; on
+// return T is uniform (the true end state when the trajectories did not merge).
 __device__ bool rerun_segment_svf(const TrigSpecArgs& a, int c, int s, const int32_t (&tap)[kFirTaps],
                                   const TrigCfg& k, TrigState& T, const TrigState& S0, int lane) {
     __shared__ TrigState t_sh;
@@ -471,48 +518,49 @@ __device__ bool rerun_segment_svf(const TrigSpecArgs& a, int c, int s, const int
         __syncthreads();
         return merged;
     }
-    const int64_t seg0 = (int64_t)s * a.L;
-    const int64_t seg1 = seg0 + a.L < a.J ? seg0 + a.L : a.J;
-    const FastCfg q = fast_cfg(k);
-    FastSvf st = to_fast_svf(lane == 0 ? T : S0);
     uint64_t* scratch = a.scratch + (int64_t)c * a.capseg;
-    int32_t nt = 0, ndrop = 0;
-    bool merged = false;
-    const int16_t* fp = a.filt + c;
-    int32_t fnext = seg0 + lane < seg1 ? (int32_t)fp[(seg0 + lane) * a.C] : 0;
-    for (int64_t g = seg0; g < seg1 && !merged; g += 64) {
-        const int32_t fl = fnext;
-        const int left = (int)(seg1 - g < 64 ? seg1 - g : 64);
-        fnext = g + 64 + lane < seg1 ? (int32_t)fp[(g + 64 + lane) * a.C] : 0;   // next block in flight
-        for (int i = 0; i < left; ++i) {
-            const int32_t f = __builtin_amdgcn_readlane(fl, i);
-            EvInfo ev;
-            const bool e = trig_update_svf(st, f, q, a.kf, a.kq, ev);
-            const uint64_t b = __ballot(e);
-            if (b & 1ull) {
-                if (lane == 0 && nt < a.capseg) scratch[nt] = make_packet(c, ev, f, a.j0 + g + i);
-                ++nt;
-            }
-            ndrop += (int32_t)((b >> 1) & 1ull);
-        }
-        auto same = [&](int32_t v) { return __builtin_amdgcn_readlane(v, 0) == __builtin_amdgcn_readlane(v, 1); };
-        merged = same((int32_t)st.low) && same((int32_t)(st.low >> 32)) && same((int32_t)st.band) &&
-                 same((int32_t)(st.band >> 32)) && same(st.x) && same(st.f1) && same(st.f2);
-    }
-    if (lane == 0) splice_segment(a, c, s, nt, ndrop, merged);
-    if (!merged) {   // lane 0's trajectory, broadcast
-        FastSvf t;
-        t.low = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(st.low >> 32), 0) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int32_t)st.low, 0));
-        t.band = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(st.band >> 32), 0) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int32_t)st.band, 0));
-        t.x = __builtin_amdgcn_readlane(st.x, 0);
-        t.f1 = __builtin_amdgcn_readlane(st.f1, 0);
-        t.f2 = __builtin_amdgcn_readlane(st.f2, 0);
-        T = from_fast_svf(t);
-    }
+    int32_t nt, ndrop;
+    TrigState Tend = T;
+    const bool merged = svf_walk(a, c, s, k, T, S0, lane, scratch, nt, ndrop, Tend);
+    if (lane == 0) splice_segment(a, c, s, nt, ndrop, merged, scratch);
+    if (!merged) T = Tend;
     __syncthreads();   // lane 0's slot and scratch writes before any later segment's re-run
     return merged;
+}
+
+// Phase A of the SVF fix-up (round 6): one wave per (channel c, segment s >= 1) of the sub-chunk.
+// A segment whose speculated start state differs from its predecessor's speculative end state is
+// re-run at once, assuming that end state is the true one (it is unless the predecessor itself
+// fails and does not merge), into its own result and packet entries; k_trig_fix confirms the
+// assumptions channel by channel and splices. The failed segments of all channels walk in parallel
+// instead of one after another in their channel's wave.
+__global__ __launch_bounds__(256) void k_trig_refix(TrigSpecArgs a) {
+    const int C = a.C;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= (int64_t)C * (a.nseg - 1)) return;   // wave-uniform
+    const int c = (int)(w % C), s = (int)(w / C) + 1;
+    const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
+    RefixRes* res = a.refix + sc;
+    const TrigState P = a.s_end[(int64_t)(s - 1) * C + c];
+    const TrigState S0 = a.s_spec[(int64_t)s * C + c];
+    int32_t status = RF_OK, nt = 0, ndrop = 0;
+    TrigState Tend = P;
+    if (!state_eq(P, S0, a.mode)) {
+        if (!P.binit || !S0.binit || in_holdoff(P) || in_holdoff(S0)) {
+            status = RF_SERIAL;   // start of stream: k_trig_fix walks it
+        } else {
+            const TrigCfg k{a.thr[c], a.rearm[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
+            status = svf_walk(a, c, s, k, P, S0, lane, a.refix_pk + sc * a.capseg, nt, ndrop, Tend) ? RF_MERGED
+                                                                                                  : RF_UNMERGED;
+        }
+    }
+    if (lane == 0) {
+        res->status = status;
+        res->nt = nt;
+        res->ndrop = ndrop;
+        res->T = Tend;
+    }
 }
 
 __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
@@ -538,9 +586,48 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
 #pragma unroll
     for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
     const TrigCfg k{a.thr[c], a.rearm[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
+    int32_t reruns = 0;
+    if (wave_walk && a.refix) {
+        // phase B after k_trig_refix: walk the segments in order. While the true start of segment s
+        // is s_end[s - 1] (truth), its phase-A result holds: OK keeps the speculative list, a re-run
+        // is spliced, an unmerged one hands its true end state on. Otherwise (T) the segment is
+        // checked against T and, if it differs, re-run here from T (phase A assumed the wrong start).
+        bool truth = true;
+        TrigState T{};
+        for (int s = 1; s < a.nseg; ++s) {
+            const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
+            const RefixRes* r = a.refix + sc;
+            const int32_t st = r->status;
+            const TrigState S0 = a.s_spec[(int64_t)s * C + c];
+            if (truth) {
+                if (st == RF_OK) continue;
+                ++reruns;
+                if (st == RF_MERGED || st == RF_UNMERGED) {
+                    if (lane == 0) splice_segment(a, c, s, r->nt, r->ndrop, st == RF_MERGED, a.refix_pk + sc * a.capseg);
+                    if (st == RF_UNMERGED) {
+                        T = r->T;
+                        truth = false;
+                    }
+                    continue;
+                }
+                T = a.s_end[(int64_t)(s - 1) * C + c];   // RF_SERIAL
+                truth = rerun_segment_svf(a, c, s, tap, k, T, S0, lane);
+            } else {
+                if (state_eq(T, S0, a.mode)) {
+                    truth = true;
+                    continue;
+                }
+                ++reruns;
+                truth = rerun_segment_svf(a, c, s, tap, k, T, S0, lane);
+            }
+        }
+        if (lane != 0) return;
+        a.st_out[c] = truth ? a.s_end[(int64_t)(a.nseg - 1) * C + c] : T;
+        if (a.reruns) a.reruns[c] = reruns;
+        return;
+    }
     TrigState T{};
     bool override_ = false;  // T holds the true start state of segment s (from an unmerged re-run)
-    int32_t reruns = 0;
     int s = 1;
     while (s < a.nseg) {
         if (!override_) {
@@ -593,6 +680,12 @@ hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s) {
         hipError_t e0 = hipGetLastError();
         if (e0 != hipSuccess) return e0;
         hipLaunchKernelGGL((k_trig_spec<MKID_BASE_SVF, true>), grid, dim3(kSpecThreads), 0, s, a);
+        if (a.refix && a.nseg > 1) {
+            hipError_t e1 = hipGetLastError();
+            if (e1 != hipSuccess) return e1;
+            const int64_t waves = (int64_t)a.C * (a.nseg - 1);
+            hipLaunchKernelGGL(k_trig_refix, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a);
+        }
     } else if (a.mode == MKID_BASE_SVF)
         hipLaunchKernelGGL(k_trig_spec<MKID_BASE_SVF>, grid, dim3(kSpecThreads), 0, s, a);
     else

@@ -93,6 +93,8 @@ struct mkid_ctx {
     float2* d_zb[2] = {nullptr, nullptr};
     int16_t* d_raw = nullptr;
     int16_t* d_filt = nullptr;      // [Jmax][C] SVF filter pre-pass output (k_mf_rows)
+    RefixRes* d_refix = nullptr;    // [C][nsub_max * nseg_max] SVF parallel re-run results (k_trig_refix)
+    uint64_t* d_refix_pk = nullptr; // [slot_cap] their true packets (the slot table's geometry)
     long long* d_ysum = nullptr;   // [C][2] fixed point 2^-kYsumFrac: sums of y' while armed
     // avgIQ accumulator (K9; startAccumulator / avgIQ_ctrl, ROACH_Setup.py:654-659): armed by
     // mkid_set_accumulator; rows accumulated since arming and the host-side sums of G c' over them
@@ -207,7 +209,7 @@ static void free_all(mkid_ctx* c) {
                     c->d_rtmp,  c->d_tstate, c->d_zb[0], c->d_zb[1], c->d_raw, c->d_filt, c->d_ysum, c->d_slots,
                     c->d_chcounts, c->d_scan, c->d_counts, c->d_in,  c->d_phase_ws, c->d_ev_ws,
                     c->d_sspec, c->d_send,  c->d_scratch, c->d_reruns, c->d_rflags, c->d_rmeans, c->d_iqtap, c->d_hcoeff,
-                    c->d_phist, c->d_phist_tmp, c->d_slot_ch};
+                    c->d_phist, c->d_phist_tmp, c->d_slot_ch, c->d_refix, c->d_refix_pk};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (auto& kt : c->pending) {
@@ -645,6 +647,10 @@ int mkid_set_baseline(mkid_ctx* c, int32_t mode, int32_t alpha, int32_t kf, int3
     if (mode == MKID_BASE_SVF && !c->d_filt) {   // the SVF filter pre-pass rows, allocated on first use
         HIPCHK(c, hipSetDevice(c->device));
         HIPCHK(c, dalloc(&c->d_filt, (size_t)c->Jmax * c->C));
+        // and the parallel re-run tables (k_trig_refix): one result per slot-table segment, one
+        // packet table the size of the slot table
+        HIPCHK(c, dalloc(&c->d_refix, (size_t)c->C * (size_t)c->ws.nsub_max * (size_t)std::max<int64_t>(1, c->ws.nseg_max)));
+        HIPCHK(c, dalloc(&c->d_refix_pk, (size_t)c->slot_cap));
     }
     c->mode = mode; c->alpha = alpha; c->kf = kf; c->kq = kq; c->base_thr = base_thr;
     return MKID_OK;
@@ -696,7 +702,7 @@ static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32
                     c->d_sspec, c->d_send,  c->d_slots, c->d_chcounts, c->d_scratch, c->d_reruns,
                     sp.J,       c->j0,      C,          sp.nseg,       sp.L,         sp.W,
                     capseg,     c->mode,    c->alpha,   c->kf,         c->kq,        c->base_thr,
-                    c->cfg.dead_time, stride, seg_off, c->d_filt};
+                    c->cfg.dead_time, stride, seg_off, c->d_filt, c->d_refix, c->d_refix_pk};
     tstart(c, MKID_K_TRIGGER, &kt, s);
     HIPCHK(c, launch_trigger(ta, s));
     tstop(c, &kt, s);

@@ -110,6 +110,16 @@ struct FrontArgs {
     const int16_t* slot_ch; // [C] k_front3 (N = 2048): channel of select slot st + 512 q (nullptr: identity)
 };
 
+// Result of one segment's parallel SVF re-run (k_trig_refix, round 6): status and, for a re-run,
+// the true packets before the merge detection (in TrigSpecArgs::refix_pk at the segment's slot
+// entry), the speculative packets the re-run dropped, and the true end state when it did not merge.
+enum { RF_OK = 0, RF_MERGED = 1, RF_UNMERGED = 2, RF_SERIAL = 3 };
+struct RefixRes {
+    int32_t status, nt, ndrop, pad;
+    TrigState T;
+};
+static_assert(sizeof(RefixRes) == 64, "RefixRes layout");
+
 struct TrigSpecArgs {
     const int16_t* raw;     // [J][C] Fix16_13 phase
     const int16_t* rhist;   // [25][C] previous call's last raw samples
@@ -134,6 +144,11 @@ struct TrigSpecArgs {
     // [J][C] matched-filter output (int16) of the SVF path's filter pre-pass (k_mf_rows), so
     // that the SVF walk, bound by one wave's instruction stream, skips the 26-tap filter
     int16_t* filt = nullptr;
+    // SVF with the pre-pass: every failed segment is re-run in parallel (k_trig_refix) assuming its
+    // predecessor's speculative end state, into [C][seg_stride] results and a [C][seg_stride][capseg]
+    // packet table; k_trig_fix then confirms the assumptions channel by channel
+    RefixRes* refix = nullptr;
+    uint64_t* refix_pk = nullptr;
 };
 
 struct HeightArgs {

@@ -312,12 +312,12 @@ int mkid_create(const mkid_cfg* cfg, int32_t device, mkid_ctx** out) {
     // tuning/test knob: pretend the GPU holds this many trigger waves (forces longer segments)
     if (const char* ev = getenv("MKID_TRIG_WAVE_SLOTS")) trig_slots = std::max<int64_t>(1, atoll(ev));
     int64_t svf_lanes = 0, svf_w = kSvfW;
-    {   // SVF segments: one per two SIMD lanes (4 SIMDs x 64 lanes per CU); test/tuning knobs
+    {   // SVF segments: one per SIMD lane (4 SIMDs x 64 lanes per CU, round 6); test/tuning knobs
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
             ncu = 256;
         c->ncu = ncu;
-        svf_lanes = (int64_t)ncu * 128;
+        svf_lanes = (int64_t)ncu * 256;
         if (const char* ev = getenv("MKID_SVF_LANES")) svf_lanes = std::max<int64_t>(1, atoll(ev));
         if (const char* ev = getenv("MKID_SVF_WARMUP"))
             svf_w = std::max<int64_t>(1, atoll(ev) / kFirTaps) * kFirTaps;

@@ -29,11 +29,13 @@ constexpr int64_t kSegL = 1024;
 constexpr int64_t kSegW = 260;
 // SVF baseline (Chamberlin 2-pole, Kf 82 / Kq 93623 Fix18_16): two integer trajectories started
 // from different states coincide only after ~10^4 samples (median 1.5e4, 99th percentile 2.9e4, max
-// 3.9e4 over 1024 simulated noisy channels; on the bench stream a 49k-sample warm-up still missed
-// 0.3 % of segments, 98k about 1 in 30000), so SVF segments speculate from kSvfW
-// samples of warm-up and are at least kSvfLmin long; lengths are multiples of 26 so that every
-// warm-up start keeps the filter ring aligned.
-constexpr int64_t kSvfW = 26 * 3780;
+// 3.9e4 over 1024 simulated noisy channels; on the bench stream a 49k-sample warm-up misses 0.3 %
+// of segments, 98k about 1 in 30000). Since round 6 the misses are re-run in
+// parallel (k_trig_refix), so the warm-up is the half length: 49 140 samples with segments at one
+// per SIMD lane (mkid_api.hip) measured 84-85 GS/s at config 3 against 65 for 98 280 at one per two
+// lanes (profiles/r06/r06{f,g}_svf_*). Lengths are multiples of 26 so that every warm-up start keeps
+// the filter ring aligned; segments are at least kSvfLmin long.
+constexpr int64_t kSvfW = 26 * 1890;
 constexpr int64_t kSvfLmin = 26 * 158;
 static_assert(kSegW % kFirTaps == 0 && kSegL >= kSegW + kFirTaps - 1, "segment geometry");
 static_assert(kSvfW % kFirTaps == 0, "SVF warm-up geometry");

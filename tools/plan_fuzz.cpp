@@ -65,7 +65,7 @@ static void fuzz_plans(int iters) {
         cfg.max_chunk = rows_max * N;
         const bool fused = rint_(0, 1) == 1;
         const int64_t trig_slots = rint_(0, 2) == 0 ? rint_(1, 64) : rint_(1, 40000);
-        const int64_t svf_lanes = rint_(0, 2) == 0 ? rint_(1, 100) : 256 * 128;
+        const int64_t svf_lanes = rint_(0, 2) == 0 ? rint_(1, 100) : (rint_(0, 1) ? 256 * 256 : 256 * 128);
         const int64_t svf_w = 26 * rint_(1, 4000);
         Workspace ws;
         const char* e = size_workspace(cfg, fused, trig_slots, svf_lanes, svf_w, ws);
@@ -138,7 +138,7 @@ static void fuzz_plans(int iters) {
 static void fuzz_sizing(int iters) {
     const int Cs[] = {256, 1024, 2048};
     const int deads[] = {0, 32, 200};
-    const int64_t trig_slots = 256 * 4 * 4, svf_lanes = 256 * 128;
+    const int64_t trig_slots = 256 * 4 * 4, svf_lanes = 256 * 256;   // an MI355X (mkid_api.hip)
     for (int it = 0; it < iters; ++it) {
         mkid_cfg cfg{};
         cfg.n_channels = Cs[rint_(0, 2)];

@@ -208,19 +208,7 @@ struct Stepper<MKID_BASE_SVF, true> {
         }
     }
     __device__ __forceinline__ bool step(int32_t f, EvInfo& ev) { return trig_update_svf(fs, f, q, kf, kq, ev); }
-    // the base-only warm-up in float64 (base_update_svf_d): begin_base / end_base convert the
-    // baseline integrators, which stay integers well inside float64's exact range
-    FastSvfD fd;
-    __device__ __forceinline__ void begin_base() { fd = FastSvfD{(double)fs.low, (double)fs.band, fs.f1, fs.f2}; }
-    __device__ __forceinline__ void step_base(int32_t f) {
-        base_update_svf_d(fd, f, q, (double)kf * 0x1p-16, (double)kq * 0x1p-16);
-    }
-    __device__ __forceinline__ void end_base() {
-        fs.low = (int64_t)fd.low;
-        fs.band = (int64_t)fd.band;
-        fs.f1 = fd.f1;
-        fs.f2 = fd.f2;
-    }
+    __device__ __forceinline__ void step_base(int32_t f) { base_update_svf(fs, f, q, kf, kq); }
     __device__ __forceinline__ TrigState state() const { return from_fast_svf(fs); }
 };
 
@@ -297,10 +285,8 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
         int32_t wbase = 0;
         if constexpr (MODE == MKID_BASE_SVF && std::is_same<std::decay_t<decltype(sp)>, Stepper<MODE, true>>::value) {
             wbase = (jw > 0 && wg > kFullWarm) ? wg - kFullWarm : 0;
-            sp.begin_base();
             run_groups(wbase, rbase, rrow, lane, (uint32_t)(2 * C),
                        [&](int32_t, int u, uint32_t r) { sp.step_base(filt(win, u, r)); });
-            sp.end_base();
         }
         run_groups(wg - wbase, rbase, rrow, lane, (uint32_t)(2 * C),
                    [&](int32_t, int u, uint32_t r) {

@@ -204,29 +204,6 @@ __device__ __forceinline__ bool trig_update_svf(FastSvf& s, int32_t f, const Fas
     return emit;
 }
 
-// The SVF baseline-only update in float64 (round 6), for the base-only part of a speculative
-// warm-up: the same integer arithmetic as base_update_svf, exact while |low|, |band|, |high| and the
-// products kf * high, kq * band stay below 2^53 (a stable filter keeps them near 2^31-2^34: products
-// < 2^52), with >> 16 as floor(x * 2^-16) and kf, kq as the dyadic doubles kf * 2^-16, kq * 2^-16.
-// One v_fma/v_mul_f64 + v_floor_f64 per product instead of the int64 v_mad_u64_u32 + v_mul_lo_u32
-// pair. Exactness is not what makes it safe: the warm-up only speculates a segment's start state,
-// which k_trig_fix compares exactly with the true one (a deviation is a failed speculation).
-struct FastSvfD {
-    double low, band;
-    int32_t f1, f2;
-};
-__device__ __forceinline__ void base_update_svf_d(FastSvfD& s, int32_t f, const FastCfg& k, double kf16, double kq16) {
-    const int32_t e = f - (int32_t)floor(s.low * 0x1p-16);
-    const bool gate = (uint32_t)e + k.goff < k.glim;
-    const double high = (double)f * 65536.0 - s.low - floor(kq16 * s.band);
-    const double band = s.band + floor(kf16 * high);
-    const double low = s.low + floor(kf16 * band);
-    s.band = gate ? band : s.band;
-    s.low = gate ? low : s.low;
-    s.f2 = s.f1;
-    s.f1 = f;
-}
-
 // Baseline-only forms for the early part of a long speculative warm-up: the baseline (EMA B /
 // SVF low, band) and the last two samples advance, the trigger state machine does not. Whatever
 // state machine code results is re-converged by the full steps of the warm-up's last part and,

@@ -79,7 +79,10 @@ def main():
     torch.cuda.synchronize()
     stream = torch.cuda.Stream(dev)          # the context and the spin kernel share it
     ch.set_stream(stream.cuda_stream)
-    spin_cycles = int(args.gap_ms * 1e-3 * 100e6)   # torch.cuda._sleep counts the 100 MHz shader clock
+    # torch.cuda._sleep's cycle count is in the GPU's own clock ticks: on the box this gave a
+    # ~0.75 ms spin for a nominal 14 ms (profiles/r06/r06c_front_gap_probe.json); the 'idle' mode
+    # is the one with the full gap
+    spin_cycles = int(args.gap_ms * 1e-3 * 100e6)
     out = {}
     for mode in ('none', 'spin', 'idle', 'svf', 'none'):
         ch.set_baseline(_lib.BASE_SVF if mode == 'svf' else _lib.BASE_EMA, 41, 82, 93623, 8192)

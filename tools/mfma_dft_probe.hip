@@ -16,7 +16,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
-#include <vector>
 
 #include "fft_common.h"
 
@@ -97,22 +96,22 @@ __global__ __launch_bounds__(1024) void stage_mfma(float2* out, int waves_per_bl
 
 static float time_kernel(void (*k)(float2*, int), float2* out, int blocks, int wpb) {
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -1.f;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(1024), 0, 0, out, wpb);   // warm-up
-    hipEventRecord(e0, 0);
+    (void)hipEventRecord(e0, 0);
     for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(1024), 0, 0, out, wpb);
-    hipEventRecord(e1, 0);
-    hipEventSynchronize(e1);
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventRecord(e1, 0);
+    float ms = -5.f;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) ms = -5.f;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return ms / 5.f;
 }
 
 int main() {
     int ncu = 0, clk_khz = 0;
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
-    hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || ncu <= 0) return 1;
+    (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
     float2* out = nullptr;
     if (hipMalloc(&out, (size_t)ncu * 1024 * sizeof(float2)) != hipSuccess) return 1;
     std::printf("{\"cus\": %d, \"iters\": %d, \"clock_mhz_attr\": %.0f", ncu, kIters, clk_khz / 1e3);
@@ -125,6 +124,6 @@ int main() {
                     wpb, tv * 1e6 / kIters, tm * 1e6 / kIters, tm / tv);
     }
     std::printf("}\n");
-    hipFree(out);
+    (void)hipFree(out);
     return 0;
 }

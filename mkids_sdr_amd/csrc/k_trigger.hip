@@ -465,22 +465,43 @@ __device__ bool svf_walk(const TrigSpecArgs& a, int c, int s, const TrigCfg& k, 
     ndrop = 0;
     bool merged = false;
     const int16_t* fp = a.filt + c;
+    // per block: each lane's emits as a bit mask (no per-row ballot and branch: the row loop is
+    // the update chain alone), the compared baselines in LDS (lanes 1-63 run the same speculative
+    // trajectory, so they store the same value), the packets assembled after the block
+    __shared__ int32_t bsh[4][2][64];
+    int32_t* bl = bsh[threadIdx.x >> 6][lane == 0 ? 0 : 1];
     int32_t fnext = seg0 + lane < seg1 ? (int32_t)fp[(seg0 + lane) * a.C] : 0;
     for (int64_t g = seg0; g < seg1 && !merged; g += 64) {
         const int32_t fl = fnext;
-        const int left = (int)(seg1 - g < 64 ? seg1 - g : 64);
+        // this block's rows arrived during the previous block: wait for them here, before the next
+        // block's load is issued (a wait inside the row loop would also wait for that load)
+        asm volatile("" ::"v"(fl));
+        const int left = __builtin_amdgcn_readfirstlane((int)(seg1 - g < 64 ? seg1 - g : 64));
         fnext = g + 64 + lane < seg1 ? (int32_t)fp[(g + 64 + lane) * a.C] : 0;   // next block in flight
+        const int32_t pf1 = __builtin_amdgcn_readlane(st.f1, 0), pf2 = __builtin_amdgcn_readlane(st.f2, 0);
+        uint64_t em = 0;
         for (int i = 0; i < left; ++i) {
             const int32_t f = __builtin_amdgcn_readlane(fl, i);
             EvInfo ev;
             const bool e = trig_update_svf(st, f, q, a.kf, a.kq, ev);
-            const uint64_t b = __ballot(e);
-            if (b & 1ull) {
-                if (lane == 0 && nt < a.capseg) out[nt] = make_packet(c, ev, f, a.j0 + g + i);
-                ++nt;
-            }
-            ndrop += (int32_t)((b >> 1) & 1ull);
+            em |= (uint64_t)e << i;
+            bl[i] = ev.base;
         }
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t e0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(em >> 32), 0) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int32_t)em, 0);
+        const uint64_t e1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(em >> 32), 1) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int32_t)em, 1);
+        ndrop += __builtin_popcountll(e1);
+        for (uint64_t m = e0; m; m &= m - 1) {   // lane 0's packets: row i, samples i - 2 .. i
+            const int i = __builtin_ctzll(m);
+            const int32_t f = __builtin_amdgcn_readlane(fl, i);
+            const int32_t y2 = i >= 1 ? __builtin_amdgcn_readlane(fl, i - 1) : pf1;
+            const int32_t y1 = i >= 2 ? __builtin_amdgcn_readlane(fl, i - 2) : (i == 1 ? pf1 : pf2);
+            if (lane == 0 && nt < a.capseg) out[nt] = make_packet(c, EvInfo{y1, y2, bsh[threadIdx.x >> 6][0][i]}, f, a.j0 + g + i);
+            ++nt;
+        }
+        __builtin_amdgcn_wave_barrier();
         auto same = [&](int32_t v) { return __builtin_amdgcn_readlane(v, 0) == __builtin_amdgcn_readlane(v, 1); };
         merged = same((int32_t)st.low) && same((int32_t)(st.low >> 32)) && same((int32_t)st.band) &&
                  same((int32_t)(st.band >> 32)) && same(st.x) && same(st.f1) && same(st.f2);

@@ -608,7 +608,7 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
     for (int i = 0; i < kFirTaps; ++i) tap[i] = a.fir[c * kFirTaps + i];
     const TrigCfg k{a.thr[c], a.rearm[c], a.mode, a.alpha, a.kf, a.kq, a.base_thr, a.dead};
     int32_t reruns = 0;
-    if (wave_walk && a.refix) {
+    if (wave_walk && a.refix && a.refix_pk) {
         // phase B after k_trig_refix: walk the segments in order. While the true start of segment s
         // is s_end[s - 1] (truth), its phase-A result holds: OK keeps the speculative list, a re-run
         // is spliced, an unmerged one hands its true end state on. Otherwise (T) the segment is
@@ -701,7 +701,7 @@ hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s) {
         hipError_t e0 = hipGetLastError();
         if (e0 != hipSuccess) return e0;
         hipLaunchKernelGGL((k_trig_spec<MKID_BASE_SVF, true>), grid, dim3(kSpecThreads), 0, s, a);
-        if (a.refix && a.nseg > 1) {
+        if (a.refix && a.refix_pk && a.nseg > 1) {
             hipError_t e1 = hipGetLastError();
             if (e1 != hipSuccess) return e1;
             const int64_t waves = (int64_t)a.C * (a.nseg - 1);

@@ -648,9 +648,18 @@ int mkid_set_baseline(mkid_ctx* c, int32_t mode, int32_t alpha, int32_t kf, int3
         HIPCHK(c, hipSetDevice(c->device));
         HIPCHK(c, dalloc(&c->d_filt, (size_t)c->Jmax * c->C));
         // and the parallel re-run tables (k_trig_refix): one result per slot-table segment, one
-        // packet table the size of the slot table
-        HIPCHK(c, dalloc(&c->d_refix, (size_t)c->C * (size_t)c->ws.nsub_max * (size_t)std::max<int64_t>(1, c->ws.nseg_max)));
-        HIPCHK(c, dalloc(&c->d_refix_pk, (size_t)c->slot_cap));
+        // packet table the size of the slot table. Both or neither (without them the fix-up walks
+        // the failed segments in the channel's wave, k_trig_fix)
+        RefixRes* rf = nullptr;
+        uint64_t* rp = nullptr;
+        hipError_t e = dalloc(&rf, (size_t)c->C * (size_t)c->ws.nsub_max * (size_t)std::max<int64_t>(1, c->ws.nseg_max));
+        if (e == hipSuccess) e = dalloc(&rp, (size_t)c->slot_cap);
+        if (e != hipSuccess) {
+            if (rf) (void)hipFree(rf);
+            FAIL(c, MKID_E_HIP, "hipMalloc of the SVF re-run tables failed");
+        }
+        c->d_refix = rf;
+        c->d_refix_pk = rp;
     }
     c->mode = mode; c->alpha = alpha; c->kf = kf; c->kq = kq; c->base_thr = base_thr;
     return MKID_OK;

@@ -61,5 +61,23 @@ __device__ __forceinline__ uint4 front_load4(const FrontArgs& a, int64_t first_h
     return *reinterpret_cast<const uint4*>(a.xhist + (s0 + a.avail + HIST));
 }
 
+// front_load4 as one unconditional load (no branch around it, so that the compiler's wait for it
+// can count the loads issued after it): the address is selected, and a load past the chunk's end
+// reads the chunk's first word and is zeroed by the caller where it is used (past)
+struct Load4 {
+    uint4 v;
+    bool past;
+};
+template <int M>
+__device__ __forceinline__ Load4 front_load4_nb(const FrontArgs& a, int64_t first_hop, int tid) {
+    constexpr int64_t HIST = (int64_t)(2 * kPfbTaps - 1 + kLpfHist) * M;
+    const int64_t s0 = first_hop * M + (int64_t)tid * 4;
+    const bool past = s0 >= a.K * M;
+    const uint32_t* p = s0 >= -a.avail ? a.x + (past ? 0 : s0) : a.xhist + (s0 + a.avail + HIST);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return Load4{make_uint4(v.x, v.y, v.z, v.w), past};
+}
+
 }  // namespace
 }  // namespace mkid

@@ -43,6 +43,9 @@ namespace {
 // transform waves (2 sub-FFTs x 4 frames) + 8 select waves (1 channel per thread), one workgroup
 // per CU. N = 512 (config 2, round 4): 4 transform waves (the 512-point FFT of each of 4 frames) +
 // 4 select waves (1 channel per thread), two workgroups per CU.
+#ifndef MKID_F3_PF2_N
+#define MKID_F3_PF2_N 512
+#endif
 template <int N>
 struct G3 {
     static constexpr int NW = N / 512;                 // sub-FFTs per frame
@@ -61,6 +64,9 @@ struct G3 {
     static constexpr size_t off_tw2 = off_tw1 + (size_t)7 * 64 * 8;
     static constexpr size_t lds_bytes = off_tw2 + (size_t)7 * 8 * 8;
     static constexpr int WG_PER_CU = 16 * 64 / BT;     // 16 waves per CU
+    // ring prefetch two iterations deep (round 6): N = 512 -2.8 ... -5.8 % in three same-box A/Bs;
+    // N = 1024 +1 %, N = 2048 +25 % (profiles/r06/r06{q,x,y}_kbench_*_pf2.log)
+    static constexpr bool PF2 = N == MKID_F3_PF2_N;
     static_assert((N == 2048 || N == 1024 || N == 512) && F * M == FW * 64 * 4 && C == SPT * CPT, "k_front3 geometry");
     static_assert(lds_bytes * WG_PER_CU <= 160 * 1024, "LDS");
 };
@@ -178,73 +184,109 @@ __global__ __launch_bounds__(G3<N>::BT, 4) void k_front3(FrontArgs a) {   // 16 
             w2[k - 1] = t2[8 * (k - 1)];
             asm volatile("" : "+v"(w1[k - 1].x), "+v"(w1[k - 1].y), "+v"(w2[k - 1].x), "+v"(w2[k - 1].y));
         }
-        for (int t = 0; t <= nit; ++t) {
-            STAMP3(0);
-            if (t < nit) {
-                const int kr = -kLpfHist + F * t;
-                // the hops iteration t + 1 adds: loaded now, written after this wave's PFB
-                const uint4 pre = front_load4<M>(a, k_b + kr + F, xt);
-                float2* reg = fbuf + ((t % G::NB) * F + slot) * G::FB + w * G::REG;
-                int sb = rb + slot;
-                sb -= sb >= RS ? RS : 0;
-                float2 v[8];
-                uint32_t xr[8][T];
+        // the transform work of iteration t: ring reads, PFB, sub-FFT, Y write
+        auto transform = [&](int t) __attribute__((always_inline)) {
+            float2* reg = fbuf + ((t % G::NB) * F + slot) * G::FB + w * G::REG;
+            int sb = rb + slot;
+            sb -= sb >= RS ? RS : 0;
+            float2 v[8];
+            uint32_t xr[8][T];
 #pragma unroll
-                for (int hi = 0; hi < 2; ++hi)
+            for (int hi = 0; hi < 2; ++hi)
 #pragma unroll
-                    for (int tau = 0; tau < T; ++tau) {
-                        int sl = sb + 2 * tau + hi;
-                        sl -= sl >= RS ? RS : 0;
-                        const uint32_t* pl = ring + sl * M + w * (M / NW) + 2 * L;
-                        const uint2 p01 = *reinterpret_cast<const uint2*>(pl);
-                        const uint2 p23 = *reinterpret_cast<const uint2*>(pl + 128);
-                        xr[4 * hi + 0][tau] = p01.x;
-                        xr[4 * hi + 1][tau] = p01.y;
-                        xr[4 * hi + 2][tau] = p23.x;
-                        xr[4 * hi + 3][tau] = p23.y;
-                    }
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    uint32_t x4[T];
-#pragma unroll
-                    for (int tau = 0; tau < T; ++tau) x4[tau] = xr[r][tau];
-                    const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermI);
-                    const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermQ);
-                    const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermI);
-                    const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermQ);
-                    int32_t ai = dot2_first(tq[r].x, i01);
-                    ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
-                    int32_t aq = dot2_first(tq[r].x, q01);
-                    aq = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(q23), aq, false);
-                    v[r] = make_float2((float)ai, (float)aq);
+                for (int tau = 0; tau < T; ++tau) {
+                    int sl = sb + 2 * tau + hi;
+                    sl -= sl >= RS ? RS : 0;
+                    const uint32_t* pl = ring + sl * M + w * (M / NW) + 2 * L;
+                    const uint2 p01 = *reinterpret_cast<const uint2*>(pl);
+                    const uint2 p23 = *reinterpret_cast<const uint2*>(pl + 128);
+                    xr[4 * hi + 0][tau] = p01.x;
+                    xr[4 * hi + 1][tau] = p01.y;
+                    xr[4 * hi + 2][tau] = p23.x;
+                    xr[4 * hi + 3][tau] = p23.y;
                 }
-                dft<8>(v);
 #pragma unroll
-                for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w1[k - 1]);
-                t1_lds(v, reg, L);
-                dft<8>(v);
+            for (int r = 0; r < 8; ++r) {
+                uint32_t x4[T];
 #pragma unroll
-                for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w2[k - 1]);
-                float2* t2w = reg + 72 * kl + la;
-                const float2* t2r = reg + 72 * kl + 9 * la;
+                for (int tau = 0; tau < T; ++tau) x4[tau] = xr[r][tau];
+                const uint32_t i01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermI);
+                const uint32_t q01 = __builtin_amdgcn_perm(x4[1], x4[0], kPermQ);
+                const uint32_t i23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermI);
+                const uint32_t q23 = __builtin_amdgcn_perm(x4[3], x4[2], kPermQ);
+                int32_t ai = dot2_first(tq[r].x, i01);
+                ai = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(i23), ai, false);
+                int32_t aq = dot2_first(tq[r].x, q01);
+                aq = __builtin_amdgcn_sdot2(as_s2(tq[r].y), as_s2(q23), aq, false);
+                v[r] = make_float2((float)ai, (float)aq);
+            }
+            dft<8>(v);
 #pragma unroll
-                for (int r = 0; r < 8; ++r) t2w[9 * r] = v[r];
-                __builtin_amdgcn_wave_barrier();
+            for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w1[k - 1]);
+            t1_lds(v, reg, L);
+            dft<8>(v);
 #pragma unroll
-                for (int r = 0; r < 8; ++r) v[r] = t2r[r];
-                dft<8>(v);
-                __builtin_amdgcn_wave_barrier();
-                float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
+            for (int k = 1; k < 8; ++k) v[k] = cmul_pk(v[k], w2[k - 1]);
+            float2* t2w = reg + 72 * kl + la;
+            const float2* t2r = reg + 72 * kl + 9 * la;
 #pragma unroll
-                for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
-                // ring refill: hops k+F .. k+2F-1 over hops k-2T-1 .. (no reader this iteration)
-                int ws = rb + 2 * T - 1 + F + qh;
+            for (int r = 0; r < 8; ++r) t2w[9 * r] = v[r];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = t2r[r];
+            dft<8>(v);
+            __builtin_amdgcn_wave_barrier();
+            float2* yw = reg + ((kl + 8 * la) ^ (la << 1));
+#pragma unroll
+            for (int r = 0; r < 8; ++r) yw[64 * r] = v[r];
+        };
+        if constexpr (!G::PF2) {
+            for (int t = 0; t <= nit; ++t) {
+                STAMP3(0);
+                if (t < nit) {
+                    const int kr = -kLpfHist + F * t;
+                    // the hops iteration t + 1 adds: loaded now, written after this wave's PFB
+                    const uint4 pre = front_load4<M>(a, k_b + kr + F, xt);
+                    transform(t);
+                    // ring refill: hops k+F .. k+2F-1 over hops k-2T-1 .. (no reader this iteration)
+                    int ws = rb + 2 * T - 1 + F + qh;
+                    ws -= ws >= RS ? RS : 0;
+                    ws -= ws >= RS ? RS : 0;
+                    ring3_put_nw<NW>(ring + ws * M, qoff, pre);
+                    rb += F;
+                    rb -= rb >= RS ? RS : 0;
+                }
+                STAMP3(1);
+                __syncthreads();
+                STAMP3(2);
+            }
+        } else {
+            // the prefetch two iterations deep, unrolled by 2 so that the two loads in flight sit in
+            // fixed registers and the wait before each refill leaves the newer one outstanding
+            // (vmcnt(1)); the loads are unconditional (past the run they read unused words)
+            auto iter = [&](int t, const Load4& use, Load4& fill) __attribute__((always_inline)) {
+                STAMP3(0);
+                const int kr = -kLpfHist + F * t;
+                fill = front_load4_nb<M>(a, k_b + kr + 2 * F, xt);   // the hops iteration t + 2 adds
+                transform(t);
+                int ws = rb + 2 * T - 1 + F + qh;   // the ring refill, as above
                 ws -= ws >= RS ? RS : 0;
                 ws -= ws >= RS ? RS : 0;
-                ring3_put_nw<NW>(ring + ws * M, qoff, pre);
+                ring3_put_nw<NW>(ring + ws * M, qoff, use.past ? make_uint4(0, 0, 0, 0) : use.v);
                 rb += F;
                 rb -= rb >= RS ? RS : 0;
+                STAMP3(1);
+                __syncthreads();
+                STAMP3(2);
+            };
+            Load4 pa = front_load4_nb<M>(a, k_b - kLpfHist + F, xt), pb;
+            int t = 0;
+            for (; t + 1 < nit; t += 2) {
+                iter(t, pa, pb);
+                iter(t + 1, pb, pa);
             }
+            if (t < nit) iter(t, pa, pb);
+            STAMP3(0);   // t = nit: the select waves' last iteration
             STAMP3(1);
             __syncthreads();
             STAMP3(2);

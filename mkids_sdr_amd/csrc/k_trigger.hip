@@ -34,6 +34,11 @@ constexpr int kSpecThreads = 256;
 // samples advance only the baseline (the SVF warm-up is ~10^5 samples, the EMA one 260)
 constexpr int32_t kFullWarm = 100;
 
+// Per-segment states (s_spec, s_end) channel-major, [c][s]: k_trig_fix's wave of channel c reads its
+// segment boundaries as consecutive entries (one coalesced load per 64 boundaries); k_trig_spec
+// writes each thread's two states once
+__device__ __forceinline__ int64_t seg_state(const TrigSpecArgs& a, int c, int s) { return (int64_t)c * a.nseg + s; }
+
 __device__ __attribute__((noinline)) uint64_t make_packet(int32_t c, EvInfo ev, int32_t f, int64_t jg) {
     return pack_wide(c, peakfit_i(ev.y1, ev.y2, f), ev.base, jg - 1);
 }
@@ -293,7 +298,7 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
                        EvInfo ev;
                        (void)sp.step(filt(win, u, r), ev);
                    });
-        if (s > 0) a.s_spec[(int64_t)s * C + c] = sp.state();
+        if (s > 0) a.s_spec[seg_state(a, c, s)] = sp.state();
         const int32_t len = (int32_t)(seg1 - seg0);
         const int32_t full = len - len % kFirTaps;
         const int32_t ng = __builtin_amdgcn_readfirstlane(full / kFirTaps);
@@ -322,7 +327,7 @@ __global__ __launch_bounds__(kSpecThreads, MKID_TRIG_MINW) void k_trig_spec(Trig
                 }
             }
         }
-        a.s_end[(int64_t)s * C + c] = sp.state();
+        a.s_end[seg_state(a, c, s)] = sp.state();
     };
     if (in_holdoff(st0)) {  // first segment after a reset: the generic recurrence
         Stepper<MODE, false> sp(st0, k, f0);
@@ -563,8 +568,8 @@ __global__ __launch_bounds__(256) void k_trig_refix(TrigSpecArgs a) {
     const int c = (int)(w % C), s = (int)(w / C) + 1;
     const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
     RefixRes* res = a.refix + sc;
-    const TrigState P = a.s_end[(int64_t)(s - 1) * C + c];
-    const TrigState S0 = a.s_spec[(int64_t)s * C + c];
+    const TrigState P = a.s_end[seg_state(a, c, s - 1)];
+    const TrigState S0 = a.s_spec[seg_state(a, c, s)];
     int32_t status = RF_OK, nt = 0, ndrop = 0;
     TrigState Tend = P;
     if (!state_eq(P, S0, a.mode)) {
@@ -588,15 +593,26 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
     extern __shared__ uint64_t okbits[];  // bit s%64 of word s/64: segment s needs no re-run
     const int c = blockIdx.x;
     const int lane = threadIdx.x;
-    const int C = a.C;
     const int nwords = (a.nseg + 63) / 64;
-    for (int wd = 0; wd < nwords; ++wd) {
-        const int s = wd * 64 + lane;
-        bool ok = true;
-        if (s >= 1 && s < a.nseg)
-            ok = state_eq(a.s_end[(int64_t)(s - 1) * C + c], a.s_spec[(int64_t)s * C + c], a.mode);
-        const uint64_t b = __ballot(ok);
-        if (lane == 0) okbits[wd] = b;
+    // four words (256 boundaries) per batch, every state loaded whole and unconditionally (clamped
+    // index; consecutive lanes read consecutive entries of the channel-major layout) so that the
+    // batch's loads are in flight together, then compared without branches
+    for (int wd0 = 0; wd0 < nwords; wd0 += 4) {
+        bool ok[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int s = (wd0 + i) * 64 + lane;
+            const bool valid = s >= 1 && s < a.nseg;
+            const int64_t ie = seg_state(a, c, valid ? s - 1 : 0), ip = seg_state(a, c, valid ? s : 0);
+            const TrigState e = a.s_end[ie];   // segment 0's entries when not valid (nseg >= 1)
+            const TrigState p = a.s_spec[ip];
+            ok[i] = !valid || state_eq_nb(e, p, a.mode);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t b = __ballot(ok[i]);
+            if (lane == 0 && wd0 + i < nwords) okbits[wd0 + i] = b;
+        }
     }
     __syncthreads();
     // SVF with the filter pre-pass: the whole wave runs the control below (uniform) and the
@@ -619,7 +635,7 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
             const int64_t sc = (int64_t)c * a.seg_stride + a.seg_off + s;
             const RefixRes* r = a.refix + sc;
             const int32_t st = r->status;
-            const TrigState S0 = a.s_spec[(int64_t)s * C + c];
+            const TrigState S0 = a.s_spec[seg_state(a, c, s)];
             if (truth) {
                 if (st == RF_OK) continue;
                 ++reruns;
@@ -631,7 +647,7 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
                     }
                     continue;
                 }
-                T = a.s_end[(int64_t)(s - 1) * C + c];   // RF_SERIAL
+                T = a.s_end[seg_state(a, c, s - 1)];   // RF_SERIAL
                 truth = rerun_segment_svf(a, c, s, tap, k, T, S0, lane);
             } else {
                 if (state_eq(T, S0, a.mode)) {
@@ -643,7 +659,7 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
             }
         }
         if (lane != 0) return;
-        a.st_out[c] = truth ? a.s_end[(int64_t)(a.nseg - 1) * C + c] : T;
+        a.st_out[c] = truth ? a.s_end[seg_state(a, c, a.nseg - 1)] : T;
         if (a.reruns) a.reruns[c] = reruns;
         return;
     }
@@ -659,19 +675,19 @@ __global__ __launch_bounds__(64) void k_trig_fix(TrigSpecArgs a) {
             if (!fail) break;
             s = wd * 64 + __builtin_ctzll(fail);
             if (s >= a.nseg) break;
-            T = a.s_end[(int64_t)(s - 1) * C + c];
-        } else if (state_eq(T, a.s_spec[(int64_t)s * C + c], a.mode)) {
+            T = a.s_end[seg_state(a, c, s - 1)];
+        } else if (state_eq(T, a.s_spec[seg_state(a, c, s)], a.mode)) {
             override_ = false;
             ++s;
             continue;
         }
         ++reruns;
-        const TrigState S0 = a.s_spec[(int64_t)s * C + c];
+        const TrigState S0 = a.s_spec[seg_state(a, c, s)];
         override_ = wave_walk ? !rerun_segment_svf(a, c, s, tap, k, T, S0, lane) : !rerun_segment(a, c, s, tap, k, T, S0);
         ++s;
     }
     if (lane != 0) return;
-    a.st_out[c] = override_ ? T : a.s_end[(int64_t)(a.nseg - 1) * C + c];
+    a.st_out[c] = override_ ? T : a.s_end[seg_state(a, c, a.nseg - 1)];
     if (a.reruns) a.reruns[c] = reruns;
 }
 

@@ -128,8 +128,8 @@ struct TrigSpecArgs {
     const int32_t* rearm;   // [C] re-arm levels (mkid_set_rearm; = thr without hysteresis)
     const TrigState* st_in; // [C] carried state (segment 0 starts from it)
     TrigState* st_out;      // [C] carried state after this call (may alias st_in)
-    TrigState* s_spec;      // [nseg][C] speculative state at each segment start
-    TrigState* s_end;       // [nseg][C] state at each segment end
+    TrigState* s_spec;      // [C][nseg] speculative state at each segment start (k_trigger.hip seg_state)
+    TrigState* s_end;       // [C][nseg] state at each segment end
     uint64_t* slots;        // [C][seg_stride][capseg] packets (entry c*seg_stride + seg_off + s)
     int32_t* counts;        // [C][seg_stride]
     uint64_t* scratch;      // [C][capseg] fix-up scratch

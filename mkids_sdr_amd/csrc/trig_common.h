@@ -232,6 +232,17 @@ __device__ __forceinline__ bool trig_step(TrigState& s, int32_t f, const TrigCfg
 // Equality of the parts of the state that influence future outputs (dead-time counter only in
 // ST_DEAD; B only for EMA; low/band only for SVF). Two trajectories with equal canonical state
 // and equal inputs produce identical packets from then on.
+// state_eq without branches, for states already in registers (k_trig_fix's check of every segment
+// boundary: with the short-circuit form each lane's later fields were loaded behind a branch, a
+// dependent memory round trip per field group)
+__device__ __forceinline__ bool state_eq_nb(const TrigState& a, const TrigState& b, int mode) {
+    bool eq = (a.binit == b.binit) & (a.st == b.st) & (a.f1 == b.f1) & (a.f2 == b.f2);
+    eq &= (a.st != ST_DEAD) | (a.cnt == b.cnt);
+    const bool base = mode == MKID_BASE_EMA ? a.B == b.B
+                                            : (mode == MKID_BASE_SVF ? (a.low == b.low) & (a.band == b.band) : true);
+    return eq & (!a.binit | base);
+}
+
 __device__ __forceinline__ bool state_eq(const TrigState& a, const TrigState& b, int mode) {
     if (a.binit != b.binit || a.st != b.st || a.f1 != b.f1 || a.f2 != b.f2) return false;
     if (a.st == ST_DEAD && a.cnt != b.cnt) return false;

@@ -8,7 +8,8 @@ namespace mkid {
 // scans the tile sums (and accumulates the call's totals), (3) per tile: block-local exclusive
 // scan + tile offset, each thread copies the packets of its EPT entries. One entry per thread:
 // with 8 the copy ran eight dependent load -> store chains in a row per thread (k_gather_events
-// 16.7 -> 8.2 us per step at config 3, 13.3 -> 5.3 us at config 2; round 6)
+// 16.7 -> 8.2 us per step at config 3, 13.3 -> 5.3 us at config 2; round 6). The block scans are
+// wave scans plus one exchange of wave totals (k_tile_scan 7.8 -> 4.8 us)
 constexpr int kCmpThreads = 256;
 constexpr int kCmpEpt = 1;                       // entries per thread
 constexpr int kCmpTile = kCmpThreads * kCmpEpt;  // entries per tile
@@ -28,21 +29,37 @@ __device__ __forceinline__ void load_counts(const int32_t* counts, int64_t n_ent
     }
 }
 
-// block-wide exclusive scan of one int64 per thread (kCmpThreads), returns the block total
-__device__ __forceinline__ int64_t block_excl_scan(int64_t x, int64_t& excl) {
-    __shared__ int64_t sm[kCmpThreads];
-    const int t = threadIdx.x;
-    sm[t] = x;
-    __syncthreads();
-    for (int off = 1; off < kCmpThreads; off <<= 1) {  // Hillis-Steele
-        const int64_t y = t >= off ? sm[t - off] : 0;
-        __syncthreads();
-        sm[t] += y;
-        __syncthreads();
+// inclusive scan over the 64 lanes of a wave (6 shuffle steps, no barrier)
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off, 64);
+        x += lane >= off ? y : 0;
     }
-    excl = sm[t] - x;
-    const int64_t tot = sm[kCmpThreads - 1];
+    return x;
+}
+
+// block-wide exclusive scan of one int64 per thread (NT threads), returns the block total: wave
+// scans, then every thread adds the totals of the waves before it (two barriers; the round-5
+// Hillis-Steele form over LDS took 2 log2(NT) barriers)
+template <int NT>
+__device__ __forceinline__ int64_t block_excl_scan(int64_t x, int64_t& excl) {
+    constexpr int NW = NT / 64;
+    __shared__ int64_t ws[NW];
+    const int w = threadIdx.x >> 6;
+    const int64_t inc = wave_incl_scan(x);
+    if ((threadIdx.x & 63) == 63) ws[w] = inc;
     __syncthreads();
+    int64_t base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const int64_t v = ws[i];
+        base += i < w ? v : 0;
+        tot += v;
+    }
+    excl = base + inc - x;
+    __syncthreads();   // ws is reused by the next scan
     return tot;
 }
 
@@ -53,8 +70,8 @@ __global__ __launch_bounds__(kCmpThreads) void k_tile_sums(const int32_t* counts
     int64_t raw, kept, ex;
     const int64_t e0 = (int64_t)blockIdx.x * kCmpTile + (int64_t)threadIdx.x * kCmpEpt;
     load_counts(counts, n_ent, e0, capseg, v, raw, kept);
-    const int64_t tk = block_excl_scan(kept, ex);
-    const int64_t tr = block_excl_scan(raw, ex);
+    const int64_t tk = block_excl_scan<kCmpThreads>(kept, ex);
+    const int64_t tr = block_excl_scan<kCmpThreads>(raw, ex);
     if (threadIdx.x == 0) {
         tile_kept[blockIdx.x] = tk;
         tile_raw[blockIdx.x] = tr;
@@ -67,31 +84,18 @@ __global__ __launch_bounds__(kCmpThreads) void k_tile_sums(const int32_t* counts
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const int64_t* tile_kept, const int64_t* tile_raw,
                                                             int64_t ntiles, int64_t cap, int64_t* tile_off,
                                                             int64_t* d_counts) {
-    __shared__ int64_t part[kScanThreads];
-    __shared__ unsigned long long tot;
-    constexpr int64_t prev = 0;
     const int64_t per = (ntiles + kScanThreads - 1) / kScanThreads;
     const int64_t b = threadIdx.x * per;
     int64_t sum = 0, sumw = 0;
     for (int64_t i = 0; i < per; ++i)
         if (b + i < ntiles) { sum += tile_raw[b + i]; sumw += tile_kept[b + i]; }
-    part[threadIdx.x] = sumw;
-    if (threadIdx.x == 0) tot = 0;
-    __syncthreads();
-    for (int off = 1; off < kScanThreads; off <<= 1) {
-        const int64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    int64_t run = prev + part[threadIdx.x] - sumw;
+    int64_t run, ex;
+    const int64_t w = block_excl_scan<kScanThreads>(sumw, run);
+    const int64_t tot = block_excl_scan<kScanThreads>(sum, ex);
     for (int64_t i = 0; i < per; ++i)
         if (b + i < ntiles) { tile_off[b + i] = run; run += tile_kept[b + i]; }
-    atomicAdd(&tot, (unsigned long long)sum);
-    __syncthreads();
     if (threadIdx.x == 0) {
-        d_counts[0] = (int64_t)tot;
-        const int64_t w = prev + part[kScanThreads - 1];
+        d_counts[0] = tot;
         d_counts[1] = w < cap ? w : cap;
     }
 }
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(kCmpThreads) void k_gather_events(const uint64_t* s
     int64_t raw, kept, ex;
     const int64_t e0 = (int64_t)blockIdx.x * kCmpTile + (int64_t)threadIdx.x * kCmpEpt;
     load_counts(counts, n_ent, e0, capseg, v, raw, kept);
-    block_excl_scan(kept, ex);
+    block_excl_scan<kCmpThreads>(kept, ex);
     int64_t o = tile_off[blockIdx.x] + ex;
 #pragma unroll
     for (int i = 0; i < kCmpEpt; ++i) {

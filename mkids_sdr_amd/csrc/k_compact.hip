@@ -5,11 +5,14 @@ namespace mkid {
 
 // ---- compaction: exclusive scan of (channel, segment) packet counts, then copy -------------
 // Three launches, all coalesced: (1) per-tile sums of TILE consecutive entries, (2) one block
-// scans the tile sums (and accumulates the call's totals), (3) per tile: block-local exclusive
-// scan + tile offset, each thread copies the packets of its EPT entries. One entry per thread:
-// with 8 the copy ran eight dependent load -> store chains in a row per thread (k_gather_events
-// 16.7 -> 8.2 us per step at config 3, 13.3 -> 5.3 us at config 2; round 6). The block scans are
-// wave scans plus one exchange of wave totals (k_tile_scan 7.8 -> 4.8 us)
+// scans the tile sums (and writes the call's totals), (3) per tile: block-local exclusive scan +
+// tile offset, each thread copies the packets of its entries; the same launch carries the call's
+// history rolls as extra blocks (round 6: one launch fewer per call). Round 6 also: one entry per
+// thread (with 8 the copy ran eight dependent load -> store chains in a row per thread:
+// k_gather_events 16.7 -> 8.2 us per step at config 3, 13.3 -> 5.3 us at config 2); the block
+// scans are wave scans plus one exchange of wave totals (k_tile_scan 7.8 -> 4.8 us); the tile scan
+// folded into (1) as a last-block pass was slower (1024 blocks serialise on the done counter:
+// k_tile_sums 4.9 -> 27 us).
 constexpr int kCmpThreads = 256;
 constexpr int kCmpEpt = 1;                       // entries per thread
 constexpr int kCmpTile = kCmpThreads * kCmpEpt;  // entries per tile
@@ -100,10 +103,36 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(const int64_t* tile_
     }
 }
 
+// ---- history roll: dst[i] = concat(old[0:hist_rows], fresh[0:fresh_rows])[fresh_rows + i] ----
+__device__ __forceinline__ void hist_roll_part(uint8_t* dst, const uint8_t* old_hist, const uint8_t* fresh,
+                                               int64_t hist_rows, int64_t fresh_rows, int64_t row_bytes,
+                                               int64_t first, int64_t stride) {
+    const int64_t total = hist_rows * row_bytes;
+    for (int64_t b = first; b < total; b += stride) {
+        const int64_t row = b / row_bytes, col = b % row_bytes;
+        const int64_t src = fresh_rows + row;  // index into concat
+        dst[b] = src < hist_rows ? old_hist[src * row_bytes + col]
+                                 : fresh[(src - hist_rows) * row_bytes + col];
+    }
+}
+
+// blocks [0, ntiles) gather; blocks after them run up to two history rolls (the call's raw-phase
+// and ADC histories, which no kernel of the call reads: one launch fewer per call)
 __global__ __launch_bounds__(kCmpThreads) void k_gather_events(const uint64_t* slots, const int32_t* counts,
                                                                int64_t n_ent, int32_t capseg,
                                                                const int64_t* tile_off, uint64_t* out,
-                                                               int64_t cap) {
+                                                               int64_t cap, int ntiles, RollJob j1, int nb1,
+                                                               RollJob j2) {
+    if ((int)blockIdx.x >= ntiles) {
+        const int rb = (int)blockIdx.x - ntiles;
+        const bool first = rb < nb1;
+        const RollJob& j = first ? j1 : j2;
+        const int64_t b0 = first ? rb : rb - nb1;
+        const int64_t nb = first ? nb1 : (int64_t)gridDim.x - ntiles - nb1;
+        hist_roll_part((uint8_t*)j.dst, (const uint8_t*)j.old_hist, (const uint8_t*)j.fresh, j.hist_rows,
+                       j.fresh_rows, j.row_bytes, b0 * blockDim.x + threadIdx.x, nb * blockDim.x);
+        return;
+    }
     int v[kCmpEpt];
     int64_t raw, kept, ex;
     const int64_t e0 = (int64_t)blockIdx.x * kCmpTile + (int64_t)threadIdx.x * kCmpEpt;
@@ -119,9 +148,16 @@ __global__ __launch_bounds__(kCmpThreads) void k_gather_events(const uint64_t* s
     }
 }
 
+static int roll_blocks(const RollJob* j) {
+    if (!j) return 0;
+    const int64_t total = j->hist_rows * j->row_bytes;
+    const int64_t b = (total + 255) / 256;
+    return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
 hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
                           int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
-                          int64_t* scan_ws, hipStream_t s) {
+                          int64_t* scan_ws, const RollJob* roll1, const RollJob* roll2, hipStream_t s) {
     // scan_ws holds n_ent int64 (>= 3 per tile)
     const int64_t ntiles = (n_ent + kCmpTile - 1) / kCmpTile;
     int64_t* tile_kept = scan_ws;
@@ -134,39 +170,18 @@ hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t 
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, s, tile_kept, tile_raw, ntiles, cap,
                        tile_off, d_counts);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_gather_events, dim3((unsigned)ntiles), dim3(kCmpThreads), 0, s, slots, counts, n_ent,
-                       capseg, tile_off, out, cap);
+    const int nb1 = roll_blocks(roll1), nb2 = roll_blocks(roll2);
+    const RollJob none{};
+    hipLaunchKernelGGL(k_gather_events, dim3((unsigned)(ntiles + nb1 + nb2)), dim3(kCmpThreads), 0, s, slots,
+                       counts, n_ent, capseg, tile_off, out, cap, (int)ntiles, roll1 ? *roll1 : none, nb1,
+                       roll2 ? *roll2 : none);
     return hipGetLastError();
-}
-
-// ---- history roll: dst[i] = concat(old[0:hist_rows], fresh[0:fresh_rows])[fresh_rows + i] ----
-__device__ __forceinline__ void hist_roll_part(uint8_t* dst, const uint8_t* old_hist, const uint8_t* fresh,
-                                               int64_t hist_rows, int64_t fresh_rows, int64_t row_bytes,
-                                               int64_t first, int64_t stride) {
-    const int64_t total = hist_rows * row_bytes;
-    for (int64_t b = first; b < total; b += stride) {
-        const int64_t row = b / row_bytes, col = b % row_bytes;
-        const int64_t src = fresh_rows + row;  // index into concat
-        dst[b] = src < hist_rows ? old_hist[src * row_bytes + col]
-                                 : fresh[(src - hist_rows) * row_bytes + col];
-    }
 }
 
 __global__ void k_hist_roll(uint8_t* dst, const uint8_t* old_hist, const uint8_t* fresh,
                             int64_t hist_rows, int64_t fresh_rows, int64_t row_bytes) {
     hist_roll_part(dst, old_hist, fresh, hist_rows, fresh_rows, row_bytes,
                    (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
-}
-
-// two rolls in one launch (the call's trigger raw-phase and ADC histories): blocks [0, nb1) roll
-// job 1, the rest job 2 — one launch and one inter-kernel gap fewer per call
-__global__ void k_hist_roll2(RollJob j1, RollJob j2, int nb1) {
-    const bool first = (int)blockIdx.x < nb1;
-    const RollJob& j = first ? j1 : j2;
-    const int64_t b0 = first ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - nb1;
-    const int64_t nb = first ? nb1 : (int64_t)gridDim.x - nb1;
-    hist_roll_part((uint8_t*)j.dst, (const uint8_t*)j.old_hist, (const uint8_t*)j.fresh, j.hist_rows,
-                   j.fresh_rows, j.row_bytes, b0 * blockDim.x + threadIdx.x, nb * blockDim.x);
 }
 
 hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
@@ -176,17 +191,6 @@ hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, 
     hipLaunchKernelGGL(k_hist_roll, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, (uint8_t*)dst,
                        (const uint8_t*)old_hist, (const uint8_t*)fresh, hist_rows, fresh_rows,
                        row_bytes);
-    return hipGetLastError();
-}
-
-hipError_t launch_hist_roll2(const RollJob& j1, const RollJob& j2, hipStream_t s) {
-    auto nblocks = [](const RollJob& j) {
-        const int64_t total = j.hist_rows * j.row_bytes;
-        const int64_t b = (total + 255) / 256;
-        return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
-    };
-    const int nb1 = nblocks(j1), nb2 = nblocks(j2);
-    hipLaunchKernelGGL(k_hist_roll2, dim3(nb1 + nb2), dim3(256), 0, s, j1, j2, nb1);
     return hipGetLastError();
 }
 

@@ -726,12 +726,14 @@ static int run_trigger(mkid_ctx* c, const int16_t* raw, const SubPlan& sp, int32
 }
 
 // K8: one compaction over the call's [C][stride] slot table -> channel-major, time-ascending.
+// Up to two history rolls ride along as extra blocks of the gather launch.
 static int compact_call(mkid_ctx* c, int32_t stride, int32_t capseg, uint64_t* d_events, int64_t cap,
-                        int64_t* d_counts, hipStream_t s) {
+                        int64_t* d_counts, hipStream_t s, const RollJob* roll1 = nullptr,
+                        const RollJob* roll2 = nullptr) {
     KTime kt;
     tstart(c, MKID_K_COMPACT, &kt, s);
     HIPCHK(c, launch_compact(c->d_slots, c->d_chcounts, (int64_t)c->C * stride, capseg, d_events, cap, d_counts,
-                             c->d_scan, s));
+                             c->d_scan, roll1, roll2, s));
     tstop(c, &kt, s);
     return MKID_OK;
 }
@@ -803,12 +805,12 @@ static int process_fused(mkid_ctx* c, const int16_t* d_iq, int64_t n, float* d_p
         c->last_subJ = J;
         c->last_raw_row = off / N;
     }
-    {
-        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, A);
+    {   // with the last sub-chunk's raw-phase history and the call's ADC history rolled in the
+        // compaction's gather launch (no kernel of the call reads the rolled-to buffers)
+        const RollJob xroll{c->d_xtmp, c->d_xhist, x, c->H, n, 4};
+        int r = compact_call(c, stride, capseg, d_events, cap, d_counts, A, &last_roll, &xroll);
         if (r) return r;
     }
-    // the last sub-chunk's raw-phase history and the call's ADC history in one launch
-    HIPCHK(c, launch_hist_roll2(last_roll, RollJob{c->d_xtmp, c->d_xhist, x, c->H, n, 4}, A));
     std::swap(c->d_rhist, c->d_rtmp);
     std::swap(c->d_xhist, c->d_xtmp);
     c->iq_rows = c->iq_ch >= 0 ? n / N : 0;

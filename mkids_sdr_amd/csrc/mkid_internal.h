@@ -175,19 +175,20 @@ hipError_t launch_front(int N, const FrontArgs& a, hipStream_t s);
 hipError_t launch_trigger(const TrigSpecArgs& a, hipStream_t s);
 // resident wave slots of the speculative trigger kernel on a device (occupancy x CUs)
 int64_t trigger_wave_slots(int device);
-hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
-                          int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
-                          int64_t* scan_ws, hipStream_t s);
+
 hipError_t launch_hist_roll(void* dst, const void* old_hist, const void* fresh, int64_t hist_rows,
                             int64_t fresh_rows, int64_t row_bytes, hipStream_t s);
-// one history-roll job (k_hist_roll's arguments); launch_hist_roll2 runs two in one launch
+// one history-roll job (k_hist_roll's arguments), for the rolls carried by the compaction launch
 struct RollJob {
     void* dst;
     const void* old_hist;
     const void* fresh;
     int64_t hist_rows, fresh_rows, row_bytes;
 };
-hipError_t launch_hist_roll2(const RollJob& j1, const RollJob& j2, hipStream_t s);
+// K8 compaction; roll1 / roll2 (or null) run as extra blocks of its gather launch
+hipError_t launch_compact(const uint64_t* slots, const int32_t* counts, int64_t n_ent,
+                          int32_t capseg, uint64_t* out, int64_t cap, int64_t* d_counts,
+                          int64_t* scan_ws, const RollJob* roll1, const RollJob* roll2, hipStream_t s);
 hipError_t launch_stream_copy(void* dst, const void* src, int64_t bytes, hipStream_t s);
 hipError_t launch_synth(int16_t* out, int64_t n, int64_t n0, const int16_t* base,
                         const mkid_synth_tone* tones, const mkid_pulse* pulses, int64_t npulses,
